@@ -1,0 +1,228 @@
+/*
+ * rt_hip.h -- C ABI of the MI355X wavefront path tracer.
+ *
+ * This is the drop-in boundary for the reference's render hot path:
+ *   camera::render(std::ofstream&, const hittable& world,
+ *                  std::shared_ptr<const hittable> light)
+ *     (/root/reference/src/camera.h:135-176)
+ * and everything it reaches per sample: camera::generate_ray (camera.h:244-284),
+ * camera::ray_color (camera.h:193-241), camera::miss (camera.h:180-190),
+ * hittable::hit for every concrete hittable (hittable.h:32-293, sphere.h:40-74,
+ * quad.h:30-52, triangle.h:27-40, volumne.h:18-46, hittable_list.h:20-31,
+ * bvh_node.h:49-59), material::{scatter,p_scattered,emitted} (material.h:36-219),
+ * pdf::{value,generate} (pdf.h:7-61, hittable_list.h:39-50) and texture::sample
+ * (texture.h:6-63).
+ *
+ * The reference has no FFI of its own: its plugin surface is the C++ virtual
+ * interfaces above. The C++ headers under
+ * cpu-ray-tracing-implementation_amd/rt/ keep those class names and
+ * constructors; each object serialises itself into an rt_scene_desc (a POD
+ * image of the hittable DAG) and camera::render hands it to this library.
+ *
+ * Conventions
+ *  - Every entry point returns rt_status; no C++ exception crosses the ABI.
+ *  - One rt_context per HIP device. A context is not re-entrant; different
+ *    contexts may be used from different host threads concurrently.
+ *  - rt_render_tiles is stream-ordered on the caller's stream (hipStream_t
+ *    passed as void*, NULL = the context's own stream) when out_rgb is a
+ *    device pointer; with a host pointer it returns after the copy.
+ *  - All geometry in the descriptor is double precision, as in the reference
+ *    (vec3.h:7). The device computes in fp32 (RT_PREC_F32, the production
+ *    path) or fp64 (RT_PREC_F64, the parity path).
+ */
+#ifndef RT_HIP_H
+#define RT_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+typedef enum rt_status {
+  RT_OK = 0,
+  RT_ERR_INVALID_ARGUMENT = 1,
+  RT_ERR_UNSUPPORTED = 2, /* scene uses a hittable/material/texture the device path does not implement */
+  RT_ERR_HIP = 3,         /* a HIP runtime call failed (message in rt_last_error) */
+  RT_ERR_OUT_OF_MEMORY = 4,
+  RT_ERR_NO_SCENE = 5,
+  RT_ERR_NO_DEVICE = 6
+} rt_status;
+
+/* ---- scene description: a POD image of the reference's hittable DAG ---- */
+
+typedef enum rt_object_kind {
+  RT_OBJ_SPHERE = 1,    /* sphere.h:7-35      a = center1, b = center2, s0 = radius, moving */
+  RT_OBJ_QUAD = 2,      /* quad.h:9-23        a = corner, b = u, c = v                     */
+  RT_OBJ_TRIANGLE = 3,  /* triangle.h:19-25   a = p0, b = p1, c = p2                       */
+  RT_OBJ_LIST = 4,      /* hittable_list.h:7-37  children[first_child .. +child_count)     */
+  RT_OBJ_BVH = 5,       /* bvh_node.h:13-47   children = the list it was built from        */
+  RT_OBJ_TRANSLATE = 6, /* hittable.h:67-89   child, a = offset                            */
+  RT_OBJ_ROTATE_X = 7,  /* hittable.h:93-158  child, s0 = sin(theta), s1 = cos(theta)      */
+  RT_OBJ_ROTATE_Y = 8,  /* hittable.h:160-225                                              */
+  RT_OBJ_ROTATE_Z = 9,  /* hittable.h:227-293                                              */
+  RT_OBJ_VOLUME = 10    /* volumne.h:9-46     child = boundary, s0 = density,
+                           material = the isotropic phase function (volumne.h:14)          */
+} rt_object_kind;
+
+typedef struct rt_object {
+  int32_t kind;        /* rt_object_kind */
+  int32_t material;    /* index into materials, or -1 */
+  int32_t child;       /* translate / rotate_* / volume: the wrapped object */
+  int32_t first_child; /* list / bvh: first index into children[] */
+  int32_t child_count; /* list / bvh: number of children */
+  int32_t moving;      /* sphere: 1 = the moving-sphere constructor (sphere.h:25-35) */
+  double a[3];
+  double b[3];
+  double c[3];
+  double s0;
+  double s1;
+} rt_object;
+
+typedef enum rt_material_kind {
+  RT_MAT_LAMBERTIAN = 1,    /* material.h:57-76   */
+  RT_MAT_METAL = 2,         /* material.h:78-97   fuzz (stored as float, material.h:96) */
+  RT_MAT_DIELECTRIC = 3,    /* material.h:100-143 refraction (float, material.h:142)    */
+  RT_MAT_ISOTROPIC = 4,     /* material.h:187-204 */
+  RT_MAT_DIFFUSE_LIGHT = 5, /* material.h:206-219 */
+  RT_MAT_GLOSS = 6          /* material.h:145-185 (not yet on the device: RT_ERR_UNSUPPORTED) */
+} rt_material_kind;
+
+typedef struct rt_material {
+  int32_t kind;    /* rt_material_kind */
+  int32_t texture; /* albedo / emission texture index */
+  float fuzz;
+  float refraction;
+  float smoothness;
+  float specular_prob;
+} rt_material;
+
+typedef enum rt_texture_kind {
+  RT_TEX_SOLID = 1,  /* texture.h:12-37 */
+  RT_TEX_CHECKER = 2 /* texture.h:39-63 */
+} rt_texture_kind;
+
+typedef struct rt_texture {
+  int32_t kind;
+  int32_t pad_;
+  double color[3]; /* solid */
+  double odd[3];   /* checker */
+  double even[3];  /* checker */
+  double scale;    /* checker */
+} rt_texture;
+
+typedef struct rt_scene_desc {
+  const rt_object* objects;
+  int32_t num_objects;
+  const int32_t* children;
+  int32_t num_children;
+  const rt_material* materials;
+  int32_t num_materials;
+  const rt_texture* textures;
+  int32_t num_textures;
+  int32_t world;      /* root object: the `world` argument of camera::render */
+  int32_t light;      /* object used for importance sampling, or -1 (camera.h:135 `light`) */
+  int32_t background; /* texture index of camera::background_, or -1 (camera.h:329) */
+  int32_t pad_;
+} rt_scene_desc;
+
+/* ---- camera: the values camera::initialize_* computes (camera.h:21-132) ---- */
+
+typedef enum rt_camera_mode {
+  RT_CAM_PERSPECTIVE = 0, /* camera.h:245-251 */
+  RT_CAM_ORTHONORMAL = 1, /* camera.h:252-258 (not yet on the device) */
+  RT_CAM_FISHEYE = 2,     /* camera.h:259-275 (not yet on the device) */
+  RT_CAM_LENS = 3         /* camera.h:276-283 (not yet on the device) */
+} rt_camera_mode;
+
+typedef struct rt_camera_desc {
+  int32_t mode;
+  int32_t image_width;
+  int32_t image_height;
+  int32_t pad_;
+  double pos[3];
+  double dir[3];
+  double right[3];
+  double up[3];
+  double viewport_width;
+  double viewport_height;
+  double focal_length;
+  double focus_dist;
+  double defocus_u[3];
+  double defocus_v[3];
+} rt_camera_desc;
+
+/* ---- rendering ---- */
+
+typedef enum rt_precision { RT_PREC_F32 = 0, RT_PREC_F64 = 1 } rt_precision;
+
+typedef struct rt_render_params {
+  int32_t spp;              /* camera::samples_per_pixel_ */
+  int32_t max_depth;        /* camera::max_recur_depth_ */
+  uint64_t seed;            /* counter-RNG key; pixel (x, y) sample s is keyed by (seed, y*W+x, s) */
+  int32_t precision;        /* rt_precision */
+  int32_t first_sample;     /* render samples [first_sample, first_sample + spp) of each pixel */
+  int32_t samples_per_item; /* samples one work item accumulates (0 = auto). Does not change the image. */
+  int32_t pool_slots;       /* wavefront pool size (0 = auto). Does not change the image. */
+} rt_render_params;
+
+/* A framebuffer rectangle. Output of a render call is the tiles packed in the
+ * given order, each row-major (top row first, camera.h:170), 3 channels per
+ * pixel: float for RT_PREC_F32, double for RT_PREC_F64. The value of a pixel
+ * is the mean over its samples (camera.h:169), identical for any tiling, any
+ * pool size and any number of GPUs. */
+typedef struct rt_tile {
+  int32_t x0;
+  int32_t y0;
+  int32_t width;
+  int32_t height;
+} rt_tile;
+
+typedef struct rt_counters {
+  uint64_t segments;   /* ray segments traced (world.hit calls, camera.h:198) */
+  uint64_t samples;    /* camera samples completed */
+  uint64_t iterations; /* extend/shade rounds of the last render */
+  uint64_t launches;   /* kernel launches of the last render */
+  double last_render_ms;
+  double extend_ms; /* device time of the extend kernels (last render, when timing enabled) */
+  double shade_ms;  /* device time of the shade kernels (last render, when timing enabled) */
+} rt_counters;
+
+typedef struct rt_context rt_context;
+
+/* Library / ABI version, for the binding to check. */
+int32_t rt_abi_version(void);
+
+/* Create a context on HIP device `device`. */
+rt_status rt_context_create(int32_t device, rt_context** out);
+void rt_context_destroy(rt_context* ctx);
+/* Message for the last failing call on ctx (or the last create failure when ctx == NULL). */
+const char* rt_last_error(const rt_context* ctx);
+
+/* Compile the hittable DAG (BVH build, instance transforms, volumes) and upload
+ * it. The library copies everything it needs; desc may be freed afterwards. */
+rt_status rt_scene_upload(rt_context* ctx, const rt_scene_desc* desc);
+
+/* Render `ntiles` rectangles of the image described by `cam`. */
+rt_status rt_render_tiles(rt_context* ctx, const rt_camera_desc* cam, const rt_render_params* params,
+                          const rt_tile* tiles, int32_t ntiles, void* out_rgb, int32_t out_is_device,
+                          void* stream);
+
+/* Counters since the last rt_reset_counters (segments, samples) and of the last render. */
+rt_status rt_stats(rt_context* ctx, rt_counters* out);
+rt_status rt_reset_counters(rt_context* ctx);
+
+/* 1 = record per-kernel device time with HIP events (slightly perturbs timing). */
+rt_status rt_set_timing(rt_context* ctx, int32_t enable);
+
+/* Counter-based RNG of the device path, evaluated on the host (for tests):
+ * returns the 32-bit draw for (seed, pixel, sample, dim). */
+uint32_t rt_rng_u32(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t dim);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_HIP_H */
