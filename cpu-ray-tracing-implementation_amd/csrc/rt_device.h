@@ -1,0 +1,511 @@
+// rt_device.h -- device-side math, RNG, intersection, traversal and shading of
+// the wavefront path tracer. Templated on the arithmetic type R (float: the
+// production path; double: the parity path that tracks the fp64 reference).
+// Each routine cites the reference code it implements.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rt_scene.h"
+
+namespace rtd {
+
+// ------------------------------------------------------------------ vectors
+template <class R>
+struct V {
+  R x, y, z;
+};
+template <class R>
+__device__ __forceinline__ V<R> mkv(R x, R y, R z) {
+  return {x, y, z};
+}
+template <class R>
+__device__ __forceinline__ V<R> ld3(const R* p) {
+  return {p[0], p[1], p[2]};
+}
+template <class R>
+__device__ __forceinline__ V<R> operator+(V<R> a, V<R> b) {
+  return {a.x + b.x, a.y + b.y, a.z + b.z};
+}
+template <class R>
+__device__ __forceinline__ V<R> operator-(V<R> a, V<R> b) {
+  return {a.x - b.x, a.y - b.y, a.z - b.z};
+}
+template <class R>
+__device__ __forceinline__ V<R> operator-(V<R> a) {
+  return {-a.x, -a.y, -a.z};
+}
+template <class R>
+__device__ __forceinline__ V<R> operator*(V<R> a, V<R> b) {
+  return {a.x * b.x, a.y * b.y, a.z * b.z};
+}
+template <class R>
+__device__ __forceinline__ V<R> operator*(R c, V<R> a) {
+  return {a.x * c, a.y * c, a.z * c};
+}
+template <class R>
+__device__ __forceinline__ V<R> operator*(V<R> a, R c) {
+  return {a.x * c, a.y * c, a.z * c};
+}
+template <class R>
+__device__ __forceinline__ V<R> operator/(V<R> a, R c) {
+  return {a.x / c, a.y / c, a.z / c};
+}
+template <class R>
+__device__ __forceinline__ R dot(V<R> a, V<R> b) {  // vec3.h:61
+  return a.x * b.x + a.y * b.y + a.z * b.z;
+}
+template <class R>
+__device__ __forceinline__ V<R> cross(V<R> a, V<R> b) {  // vec3.h:79-82
+  return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+template <class R>
+__device__ __forceinline__ R len(V<R> a) {
+  return sqrt(a.x * a.x + a.y * a.y + a.z * a.z);
+}
+template <class R>
+__device__ __forceinline__ V<R> unit(V<R> a) {  // vec3.h:77
+  return a / len(a);
+}
+template <class R>
+__device__ __forceinline__ V<R> reflect(V<R> v, V<R> n) {  // utility.h:70
+  return v - (R(2) * dot(v, n)) * n;
+}
+template <class R>
+__device__ __forceinline__ V<R> refract(V<R> v, V<R> n, R eta) {  // utility.h:71-76
+  R cos_theta = fmin(dot(-v, n), R(1));
+  V<R> perp = eta * (v + cos_theta * n);
+  V<R> par = (-sqrt(fabs(R(1) - dot(perp, perp)))) * n;
+  return perp + par;
+}
+
+template <class R>
+struct Num;
+template <>
+struct Num<float> {
+  static constexpr float inf() { return __builtin_huge_valf(); }
+  static constexpr float pi() { return 3.14159265358979323846f; }
+  static constexpr float box_slack() { return 1.0f + 2.0f * 3.0f * 5.9604645e-08f; }  // 1 + 2*gamma(3)
+};
+template <>
+struct Num<double> {
+  static constexpr double inf() { return __builtin_huge_val(); }
+  static constexpr double pi() { return 3.1415926535897932385; }  // utility.h:15
+  static constexpr double box_slack() { return 1.0 + 2.0 * 3.0 * 1.1102230246251565e-16; }
+};
+
+// ------------------------------------------------------------------ counter RNG
+// 32-bit draw for (seed, pixel, sample, dim); identical to the oracle's
+// (oracle/oracle.cpp) and to rt_rng_u32 on the host.
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x21f0aaadu;
+  x ^= x >> 15;
+  x *= 0xd35a2d97u;
+  x ^= x >> 15;
+  return x;
+}
+__host__ __device__ __forceinline__ uint32_t key_pixel(uint64_t seed, uint32_t pixel) {
+  return mix32(pixel ^ mix32((uint32_t)seed ^ 0x9E3779B9u));
+}
+__host__ __device__ __forceinline__ uint32_t key_sample(uint64_t seed, uint32_t sample) {
+  return mix32(sample + mix32((uint32_t)(seed >> 32) + 0x7F4A7C15u));
+}
+__host__ __device__ __forceinline__ uint32_t draw_u32(uint32_t ka, uint32_t kb, uint32_t dim) {
+  return mix32(ka ^ mix32(kb + dim * 0x9E3779B9u));
+}
+template <class R>
+__device__ __forceinline__ R to_unit(uint32_t x) {  // exact 24-bit value in [0,1)
+  return R(x >> 8) * R(1.0 / 16777216.0);
+}
+// draw dimensions: camera 0..2; bounce b: 3 + 16 b + j,
+// j in [0,12) volume draws (volumne.h:36), j in [12,16) scatter/pdf draws.
+constexpr uint32_t kDimsCamera = 3, kDimsPerBounce = 16, kVolumeSlots = 12;
+__device__ __forceinline__ uint32_t dim_volume(uint32_t bounce, uint32_t j) {
+  return kDimsCamera + kDimsPerBounce * bounce + (j < kVolumeSlots ? j : kVolumeSlots - 1);
+}
+__device__ __forceinline__ uint32_t dim_scatter(uint32_t bounce, uint32_t j) {
+  return kDimsCamera + kDimsPerBounce * bounce + kVolumeSlots + (j < 4u ? j : 3u);
+}
+
+struct Keys {
+  uint32_t ka, kb;
+};
+
+// ------------------------------------------------------------------ scene view
+template <class R>
+struct DevScene {
+  const Quad<R>* quads;
+  const Sphere<R>* spheres;
+  const Tri<R>* tris;
+  const Instance<R>* insts;
+  const Volume<R>* vols;
+  const Node<R>* nodes;
+  const uint32_t* refs;
+  const Material<R>* mats;
+  const Texture<R>* texs;
+  const Light<R>* light;
+  uint32_t root;
+  int32_t background;
+  int32_t has_volumes;
+  int32_t pad;
+};
+
+// World -> object through an instance chain (hittable.h:75-82, 125-135, 192-202, 259-270).
+template <class R>
+__device__ __forceinline__ V<R> op_in(const XOp<R>& op, V<R> p, bool point) {
+  if (op.kind == 0) {
+    if (point) p = mkv(p.x - op.x, p.y - op.y, p.z - op.z);
+    return p;
+  }
+  const R s = op.x, c = op.y;
+  if (op.kind == 1) return mkv(p.x, c * p.y - s * p.z, s * p.y + c * p.z);  // rotate_x
+  if (op.kind == 2) return mkv(c * p.x - s * p.z, p.y, s * p.x + c * p.z);  // rotate_y
+  return mkv(c * p.x - s * p.y, s * p.x + c * p.y, p.z);                    // rotate_z
+}
+// Object -> world for a hit point or normal (hittable.h:80, 138-147, 205-214, 273-282).
+template <class R>
+__device__ __forceinline__ V<R> op_out(const XOp<R>& op, V<R> p, bool point) {
+  if (op.kind == 0) {
+    if (point) p = mkv(p.x + op.x, p.y + op.y, p.z + op.z);
+    return p;
+  }
+  const R s = op.x, c = op.y;
+  if (op.kind == 1) return mkv(p.x, c * p.y + s * p.z, -s * p.y + c * p.z);
+  if (op.kind == 2) return mkv(c * p.x + s * p.z, p.y, -s * p.x + c * p.z);
+  return mkv(c * p.x + s * p.y, -s * p.x + c * p.y, p.z);
+}
+template <class R>
+__device__ __forceinline__ void chain_in(const Instance<R>& in, V<R>& o, V<R>& d) {
+  for (int k = 0; k < in.nops; k++) {
+    o = op_in(in.op[k], o, true);
+    d = op_in(in.op[k], d, false);
+  }
+}
+
+// ------------------------------------------------------------------ primitive tests
+// Ray/box slab test with IEEE min/max (a NaN slab is ignored: conservative) and
+// the robust 1 + 2*gamma(3) widening of the exit distance.
+template <class R>
+__device__ __forceinline__ bool box_hit(const R* lo, const R* hi, V<R> o, V<R> inv, R tmin, R tmax, R& tnear) {
+  R tx0 = (lo[0] - o.x) * inv.x, tx1 = (hi[0] - o.x) * inv.x;
+  R ty0 = (lo[1] - o.y) * inv.y, ty1 = (hi[1] - o.y) * inv.y;
+  R tz0 = (lo[2] - o.z) * inv.z, tz1 = (hi[2] - o.z) * inv.z;
+  R tn = fmax(fmax(fmin(tx0, tx1), fmin(ty0, ty1)), fmax(fmin(tz0, tz1), tmin));
+  R tf = fmin(fmin(fmax(tx0, tx1), fmax(ty0, ty1)), fmin(fmax(tz0, tz1), tmax)) * Num<R>::box_slack();
+  tnear = tn;
+  return tn <= tf;
+}
+
+// quad::hit (quad.h:30-52) with the alpha/beta triple products precomputed.
+template <class R>
+__device__ __forceinline__ bool quad_t(const Quad<R>& q, V<R> o, V<R> d, R tmin, R tmax, R& t) {
+  V<R> n = ld3(q.n);
+  R th = (q.D - dot(n, o)) / dot(n, d);
+  if (!(tmin <= th && th <= tmax)) return false;  // interval::is_contains, NaN fails
+  V<R> p = (o + th * d) - ld3(q.q);
+  R a = dot(p, ld3(q.a)), b = dot(p, ld3(q.b));
+  if (!(R(0) <= a && a <= R(1) && R(0) <= b && b <= R(1))) return false;  // quad.h:58-64
+  t = th;
+  return true;
+}
+
+// triangle::hit / moller_trumbore (triangle.h:8-40).
+template <class R>
+__device__ __forceinline__ bool tri_t(const Tri<R>& tr, V<R> o, V<R> d, R tmin, R tmax, R& t) {
+  V<R> e1 = ld3(tr.e1), e2 = ld3(tr.e2);
+  V<R> s = o - ld3(tr.p0);
+  V<R> s1 = cross(d, e2), s2 = cross(s, e1);
+  R den = dot(s1, e1);
+  R th = dot(s2, e2) / den, b0 = dot(s1, s) / den, b1 = dot(s2, d) / den;
+  if (th < tmin || th > tmax) return false;
+  if (b0 < R(0) || b1 < R(0) || b0 + b1 > R(1)) return false;
+  if (th != th) return false;  // 0/0 determinant: the reference's comparisons reject NaN too
+  t = th;
+  return true;
+}
+
+// sphere::hit (sphere.h:40-74). `far_only` is used for the sphere the ray
+// starts on: in exact arithmetic its near root is 0 (rejected by the 0.001
+// interval) and the ray re-enters only if it points inside.
+template <class T>
+__device__ __forceinline__ bool sphere_roots(T ox, T oy, T oz, T dx, T dy, T dz, T cx, T cy, T cz, T r, T tmin,
+                                             T tmax, bool far_only, T& t) {
+  T fx = ox - cx, fy = oy - cy, fz = oz - cz;
+  T a = dx * dx + dy * dy + dz * dz;
+  T b = T(2) * (dx * fx + dy * fy + dz * fz);
+  T c = (fx * fx + fy * fy + fz * fz) - r * r;
+  T disc = b * b - T(4) * a * c;
+  if (disc < T(0)) return false;
+  T sq = sqrt(disc);
+  T root = (-b - sq) / (T(2) * a);
+  if (far_only || !(tmin <= root && root <= tmax)) {
+    root = (-b + sq) / (T(2) * a);
+    if (!(tmin <= root && root <= tmax)) return false;
+  }
+  t = root;
+  return true;
+}
+
+template <class R>
+__device__ __forceinline__ V<R> sphere_center(const Sphere<R>& s, R time) {  // sphere.h:83
+  V<R> c = ld3(s.c1);
+  if (s.moving) c = c + time * ld3(s.dc);
+  return c;
+}
+
+template <class R>
+__device__ __forceinline__ bool sphere_t(const Sphere<R>& s, V<R> o, V<R> d, R time, R tmin, R tmax, bool self, R& t) {
+  V<R> c = sphere_center(s, time);
+  bool far_only = false;
+  if (self) {
+    if (dot(d, o - c) >= R(0)) return false;  // leaving the sphere it starts on
+    far_only = true;
+  }
+  if (sizeof(R) == 4 && s.r > R(16)) {
+    // big spheres (the RTOW ground, r = 1000): |o-c|^2 - r^2 cancels catastrophically in fp32
+    double td;
+    if (!sphere_roots<double>(o.x, o.y, o.z, d.x, d.y, d.z, c.x, c.y, c.z, s.r, tmin, tmax, far_only, td))
+      return false;
+    t = (R)td;
+    return true;
+  }
+  return sphere_roots<R>(o.x, o.y, o.z, d.x, d.y, d.z, c.x, c.y, c.z, s.r, tmin, tmax, far_only, t);
+}
+
+// Closest hit over a primitive list (refs until END); used for volume boundaries.
+template <class R>
+__device__ bool list_closest(const DevScene<R>& sc, uint32_t pos, V<R> o, V<R> d, R time, R tmin, R tmax, R& t) {
+  bool any = false;
+  for (;; pos++) {
+    uint32_t e = sc.refs[pos];
+    if (e == kEnd) break;
+    uint32_t ty = etype(e), i = epay(e);
+    R th;
+    bool h = false;
+    if (ty == E_QUAD)
+      h = quad_t(sc.quads[i], o, d, tmin, tmax, th);
+    else if (ty == E_SPHERE)
+      h = sphere_t(sc.spheres[i], o, d, time, tmin, tmax, false, th);
+    else if (ty == E_TRI)
+      h = tri_t(sc.tris[i], o, d, tmin, tmax, th);
+    if (h) {
+      any = true;
+      tmax = th;
+      t = th;
+    }
+  }
+  return any;
+}
+
+// volumne::hit (volumne.h:18-46). o, d: the ray as the volume sees it.
+template <class R>
+__device__ bool volume_t(const DevScene<R>& sc, const Volume<R>& v, V<R> o, V<R> d, R time, R tmin, R tmax, Keys k,
+                         uint32_t bounce, uint32_t& jv, R& t) {
+  V<R> bo = o, bd = d;
+  if (v.inst >= 0) {
+    // the boundary chain is absolute (world -> boundary); volumes live at the level their chain starts
+    // from, which the compiler guarantees is the world for top-level volumes.
+    chain_in(sc.insts[v.inst], bo, bd);
+  }
+  R t1, t2;
+  if (!list_closest(sc, epay(v.boundary), bo, bd, time, -Num<R>::inf(), Num<R>::inf(), t1)) return false;
+  if (!list_closest(sc, epay(v.boundary), bo, bd, time, t1 + R(0.0001), Num<R>::inf(), t2)) return false;
+  if (t1 < tmin) t1 = tmin;
+  if (t2 > tmax) t2 = tmax;
+  if (t1 >= t2) return false;
+  if (t1 < R(0)) t1 = R(0);
+  R rl = len(d);
+  R inside = (t2 - t1) * rl;
+  R u = to_unit<R>(draw_u32(k.ka, k.kb, dim_volume(bounce, jv++)));
+  R hd = v.neg_inv_density * log(u);
+  if (hd > inside) return false;
+  t = t1 + hd / rl;
+  return true;
+}
+
+// ------------------------------------------------------------------ traversal
+// world.hit(r, interval(0.001, inf), rec) (camera.h:198) as a stack machine.
+// excl_*: the surface the ray leaves (its previous hit); a planar primitive
+// cannot be re-hit from its own surface, a sphere only through its far side.
+template <class R, int STACK, int BLOCK>
+__device__ void trace(const DevScene<R>& sc, V<R> wo, V<R> wd, R time, uint32_t excl_e, int32_t excl_i, Keys keys,
+                      uint32_t bounce, uint32_t* stk, R& t_best, uint32_t& e_best, int32_t& i_best) {
+  const R tmin = R(0.001);
+  R tmax = Num<R>::inf();
+  V<R> o = wo, d = wd;
+  V<R> inv = mkv(R(1) / d.x, R(1) / d.y, R(1) / d.z);
+  int32_t cur = -1;
+  uint32_t jv = 0;
+  int sp = 0;
+  e_best = kNoHit;
+  i_best = -1;
+  stk[0] = sc.root;
+  sp = 1;
+
+  auto test_prim = [&](uint32_t e) {
+    uint32_t ty = etype(e), i = epay(e);
+    bool self = (e == excl_e) && (cur == excl_i);
+    R th;
+    bool h;
+    if (ty == E_QUAD) {
+      if (self) return;
+      h = quad_t(sc.quads[i], o, d, tmin, tmax, th);
+    } else if (ty == E_SPHERE) {
+      h = sphere_t(sc.spheres[i], o, d, time, tmin, tmax, self, th);
+    } else {
+      if (self) return;
+      h = tri_t(sc.tris[i], o, d, tmin, tmax, th);
+    }
+    if (h) {
+      tmax = th;
+      e_best = e;
+      i_best = cur;
+    }
+  };
+  auto test_volume = [&](uint32_t e) {
+    R th;
+    if (volume_t(sc, sc.vols[epay(e)], o, d, time, tmin, tmax, keys, bounce, jv, th)) {
+      tmax = th;
+      e_best = e;
+      i_best = cur;
+    }
+  };
+
+  while (sp > 0) {
+    uint32_t e = stk[(--sp) * BLOCK];
+    uint32_t ty = etype(e);
+    if (ty == E_NODE) {
+      const Node<R>& nd = sc.nodes[epay(e)];
+      R t0, t1;
+      bool h0 = box_hit(nd.lo[0], nd.hi[0], o, inv, tmin, tmax, t0);
+      bool h1 = box_hit(nd.lo[1], nd.hi[1], o, inv, tmin, tmax, t1);
+      uint32_t c0 = nd.child[0], c1 = nd.child[1];
+      if (h0 && h1) {
+        if (t1 < t0) {
+          uint32_t tmp = c0;
+          c0 = c1;
+          c1 = tmp;
+        }
+        stk[(sp++) * BLOCK] = c1;  // far first, near on top
+        stk[(sp++) * BLOCK] = c0;
+      } else if (h0) {
+        stk[(sp++) * BLOCK] = c0;
+      } else if (h1) {
+        stk[(sp++) * BLOCK] = c1;
+      }
+    } else if (ty == E_LIST) {
+      uint32_t pos = epay(e);
+      for (;;) {
+        uint32_t r = sc.refs[pos];
+        if (r == kEnd) break;
+        uint32_t rt = etype(r);
+        if (rt <= E_TRI) {
+          test_prim(r);
+        } else if (rt == E_VOLUME) {
+          test_volume(r);
+        } else {
+          if (sc.refs[pos + 1] != kEnd) stk[(sp++) * BLOCK] = mk(E_LIST, pos + 1);
+          stk[(sp++) * BLOCK] = r;
+          break;
+        }
+        pos++;
+      }
+    } else if (ty <= E_TRI) {
+      test_prim(e);
+    } else if (ty == E_INSTANCE) {
+      const Instance<R>& in = sc.insts[epay(e)];
+      stk[(sp++) * BLOCK] = kRestoreBase + (uint32_t)(cur + 1);
+      stk[(sp++) * BLOCK] = in.blas;
+      cur = (int32_t)epay(e);
+      o = wo;
+      d = wd;
+      chain_in(in, o, d);
+      inv = mkv(R(1) / d.x, R(1) / d.y, R(1) / d.z);
+    } else if (ty == E_VOLUME) {
+      test_volume(e);
+    } else {  // RESTORE(k)
+      cur = (int32_t)(e - kRestoreBase) - 1;
+      o = wo;
+      d = wd;
+      if (cur >= 0) chain_in(sc.insts[cur], o, d);
+      inv = mkv(R(1) / d.x, R(1) / d.y, R(1) / d.z);
+    }
+  }
+  t_best = tmax;
+}
+
+// ------------------------------------------------------------------ textures, pdfs
+template <class R>
+__device__ __forceinline__ V<R> tex_sample(const Texture<R>& tx, V<R> p) {  // texture.h:15,47-56
+  if (tx.kind == T_SOLID) return ld3(tx.c0);
+  V<R> uv = p / tx.scale;
+  int total = (int)floor(uv.x) + (int)floor(uv.y) + (int)floor(uv.z);
+  return (total % 2 == 0) ? ld3(tx.c1) : ld3(tx.c0);
+}
+
+template <class R>
+struct Onb {  // onb.h:18-29
+  V<R> x, y, z;
+};
+template <class R>
+__device__ __forceinline__ Onb<R> make_onb(V<R> n) {
+  Onb<R> b;
+  b.y = unit(n);
+  V<R> a = (fabs(b.y.x) > R(0.9)) ? mkv(R(0), R(0), R(1)) : mkv(R(1), R(0), R(0));
+  b.z = unit(cross(b.y, a));
+  b.x = cross(b.y, b.z);
+  return b;
+}
+template <class R>
+__device__ __forceinline__ V<R> onb_transform(const Onb<R>& b, V<R> v) {  // onb.h:6
+  V<R> r = mkv(R(0), R(0), R(0));
+  r = r + v.x * b.x;
+  r = r + v.y * b.y;
+  r = r + v.z * b.z;
+  return r;
+}
+// random_in_unit_sphere (utility.h:30-42): a point ON the unit sphere
+template <class R>
+__device__ __forceinline__ V<R> on_sphere(R u1, R u2) {
+  R cos_theta = R(1) - R(2) * u1;
+  R sin_theta = sqrt(R(1) - cos_theta * cos_theta);
+  R phi = R(2) * Num<R>::pi() * u2;
+  return mkv(sin_theta * cos(phi), cos_theta, sin_theta * sin(phi));
+}
+// random_cosine_direction (utility.h:61-69)
+template <class R>
+__device__ __forceinline__ V<R> cosine_dir(R r1, R r2) {
+  R phi = R(2) * Num<R>::pi() * r1;
+  R sr2 = sqrt(r2);
+  return mkv(cos(phi) * sr2, sqrt(R(1) - r2), sin(phi) * sr2);
+}
+
+// hittable_pdf over the light (hittable_list.h:39-50 -> quad.h:66-78 / sphere.h:76-81 / hittable.h:39-41)
+template <class R>
+__device__ __forceinline__ R light_pdf(const Light<R>& L, V<R> o, V<R> dir) {
+  if (L.kind == L_QUAD) {
+    R t;
+    if (!quad_t(L.quad, o, dir, R(0.001), Num<R>::inf(), t)) return R(0);
+    R dist2 = t * t * dot(dir, dir);
+    R cosine = fabs(dot(unit(dir), ld3(L.quad.n)));
+    return dist2 / (cosine * L.quad.area);
+  }
+  if (L.kind == L_SPHERE) {
+    V<R> f = o - ld3(L.center);
+    return L.radius * L.radius * Num<R>::pi() / dot(f, f);
+  }
+  return R(0);
+}
+template <class R>
+__device__ __forceinline__ V<R> light_random(const Light<R>& L, V<R> o, R u1, R u2) {
+  if (L.kind == L_QUAD) {
+    V<R> p = (ld3(L.quad.q) + u1 * ld3(L.u)) + u2 * ld3(L.v);
+    return p - o;
+  }
+  if (L.kind == L_SPHERE) return on_sphere(u1, u2) * L.radius;
+  return mkv(R(1), R(0), R(0));
+}
+
+}  // namespace rtd

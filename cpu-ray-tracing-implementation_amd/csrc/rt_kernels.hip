@@ -1,0 +1,864 @@
+// rt_kernels.hip -- wavefront path tracer for MI355X (gfx950) + the C ABI of include/rt_hip.h.
+//
+// The reference's per-pixel/per-sample loop (camera.h:154-172) and recursive
+// ray_color (camera.h:193-241) become a pool of P path slots held in HBM as
+// structure-of-arrays (16-byte records per slot, coalesced dwordx4 access):
+//
+//   k_init    first camera ray of every slot            (camera.h:244-251)
+//   repeat:
+//     k_extend  closest hit of every live ray            (camera.h:198, world.hit)
+//     k_shade   emission + scatter + mixture pdf, or     (camera.h:199-240)
+//               finish the sample and regenerate the next camera ray of the
+//               slot's work item (pixel, chunk of samples)
+//     every kBatch rounds: k_count/k_scan/k_compact build the live-slot queue
+//     (wave __ballot + block prefix sums) once half the pool has drained
+//   k_resolve  per-pixel mean over the chunks, in chunk order (camera.h:169-170)
+//
+// Work item = (pixel, chunk of C consecutive samples); slot s owns items
+// s, s + P, s + 2P, ... Each sample's random numbers are keyed by
+// (seed, global pixel, sample) so the image is bit-identical for any pool size,
+// tiling or GPU count.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_hip.h"
+#include "rt_device.h"
+#include "scene_compile.h"
+
+using namespace rtd;
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kBatch = 16;           // extend/shade rounds between live-slot counts
+constexpr int kSegShards = 256;      // segment counter shards
+constexpr uint32_t kAutoPool32 = 1u << 20;
+constexpr uint32_t kAutoPool64 = 1u << 19;
+constexpr uint32_t kAutoChunk = 16;
+
+template <class R>
+struct alignas(4 * sizeof(R)) R4 {
+  R x, y, z, w;
+};
+template <class R>
+struct alignas(16) HitRec {
+  R t;
+  uint32_t e;
+  int32_t i;
+};
+
+template <class R>
+struct Params {
+  DevScene<R> sc;
+  R4<R>* O;      // origin, time
+  R4<R>* D;      // direction, bounce (-1 = slot finished)
+  HitRec<R>* H;  // closest hit of the current segment / surface the ray leaves
+  R4<R>* T;      // path throughput
+  R4<R>* L;      // radiance of the current sample
+  R4<R>* A;      // sum of the finished samples of the current item
+  uint4* S;      // key_pixel, key_sample, item, sample (0-based within the pixel)
+  R* partial;    // per item: 3 sums
+  const uint32_t* pixmap;  // local pixel -> global pixel id y*W + x
+  const uint32_t* queue;   // live slots, or null = slots [0, n)
+  uint32_t n;
+  uint32_t P, npix, n_items, chunk, spp, first_sample, W;
+  int32_t max_depth;
+  uint64_t seed;
+  V<R> pos, du, dv, dir00;
+  unsigned long long* seg_shards;
+};
+
+// ------------------------------------------------------------------ camera ray (camera.h:244-251,293)
+template <class R>
+__device__ __forceinline__ void camera_ray(const Params<R>& p, uint32_t gpix, Keys k, V<R>& o, V<R>& d, R& tm) {
+  uint32_t x = gpix % p.W, y = gpix / p.W;
+  V<R> rd = (p.dir00 + R(x) * p.du) + R(y) * p.dv;
+  R ox = to_unit<R>(draw_u32(k.ka, k.kb, 0)) - R(0.5);
+  R oy = to_unit<R>(draw_u32(k.ka, k.kb, 1)) - R(0.5);
+  d = (rd + ox * p.du) + oy * p.dv;
+  tm = to_unit<R>(draw_u32(k.ka, k.kb, 2));
+  o = p.pos;
+}
+
+template <class R>
+__device__ __forceinline__ void begin_sample(const Params<R>& p, uint32_t slot, uint32_t item, uint32_t sample,
+                                             R4<R> acc) {
+  uint32_t gpix = p.pixmap[item % p.npix];
+  Keys k{key_pixel(p.seed, gpix), key_sample(p.seed, p.first_sample + sample)};
+  V<R> o, d;
+  R tm;
+  camera_ray(p, gpix, k, o, d, tm);
+  p.O[slot] = {o.x, o.y, o.z, tm};
+  p.D[slot] = {d.x, d.y, d.z, R(0)};
+  p.T[slot] = {R(1), R(1), R(1), R(0)};
+  p.L[slot] = {R(0), R(0), R(0), R(0)};
+  p.A[slot] = acc;
+  p.S[slot] = make_uint4(k.ka, k.kb, item, sample);
+  HitRec<R> h;
+  h.t = R(0);
+  h.e = kNoHit;
+  h.i = -1;
+  p.H[slot] = h;
+}
+
+template <class R>
+__global__ __launch_bounds__(kBlock) void k_init(Params<R> p) {
+  uint32_t slot = blockIdx.x * kBlock + threadIdx.x;
+  if (slot >= p.P) return;
+  if (slot >= p.n_items) {
+    p.D[slot] = {R(0), R(0), R(0), R(-1)};
+    return;
+  }
+  uint32_t item = slot;
+  begin_sample(p, slot, item, (item / p.npix) * p.chunk, R4<R>{R(0), R(0), R(0), R(0)});
+}
+
+// ------------------------------------------------------------------ extend
+template <class R, int STACK>
+__global__ __launch_bounds__(kBlock) void k_extend(Params<R> p) {
+  __shared__ uint32_t stk[STACK * kBlock];
+  __shared__ uint32_t wave_cnt[kBlock / 64];
+  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  bool active = i < p.n;
+  uint32_t slot = 0;
+  R4<R> Dv{};
+  if (active) {
+    slot = p.queue ? p.queue[i] : i;
+    Dv = p.D[slot];
+    active = Dv.w >= R(0);
+  }
+  if (active) {
+    R4<R> Ov = p.O[slot];
+    HitRec<R> prev = p.H[slot];
+    Keys k{0, 0};
+    if (p.sc.has_volumes) {
+      uint4 s = p.S[slot];
+      k = {s.x, s.y};
+    }
+    R t;
+    uint32_t e;
+    int32_t inst;
+    trace<R, STACK, kBlock>(p.sc, mkv(Ov.x, Ov.y, Ov.z), mkv(Dv.x, Dv.y, Dv.z), Ov.w, prev.e, prev.i, k,
+                            (uint32_t)Dv.w, stk + threadIdx.x, t, e, inst);
+    HitRec<R> h;
+    h.t = t;
+    h.e = e;
+    h.i = inst;
+    p.H[slot] = h;
+  }
+  // segments traced: one count per wave, one atomic per block
+  unsigned long long m = __ballot(active);
+  int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) wave_cnt[wave] = (uint32_t)__popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t c = 0;
+    for (int w = 0; w < kBlock / 64; w++) c += wave_cnt[w];
+    if (c) atomicAdd(&p.seg_shards[blockIdx.x % kSegShards], (unsigned long long)c);
+  }
+}
+
+// ------------------------------------------------------------------ shade
+template <class R>
+__global__ __launch_bounds__(kBlock) void k_shade(Params<R> p) {
+  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= p.n) return;
+  uint32_t slot = p.queue ? p.queue[i] : i;
+  R4<R> Dv = p.D[slot];
+  if (Dv.w < R(0)) return;
+  const DevScene<R>& sc = p.sc;
+  R4<R> Ov = p.O[slot];
+  HitRec<R> h = p.H[slot];
+  R4<R> Tv = p.T[slot];
+  uint4 S = p.S[slot];
+  Keys k{S.x, S.y};
+  uint32_t bounce = (uint32_t)Dv.w;
+  V<R> o = mkv(Ov.x, Ov.y, Ov.z), d = mkv(Dv.x, Dv.y, Dv.z);
+  R tm = Ov.w;
+  V<R> thr = mkv(Tv.x, Tv.y, Tv.z);
+  V<R> add = mkv(R(0), R(0), R(0));
+  bool has_add = false, done = false;
+  V<R> new_o = o, new_d = d;
+
+  if (h.e == kNoHit) {  // camera::miss (camera.h:180-190)
+    if (sc.background >= 0) {
+      R t;
+      if (sphere_roots<R>(o.x, o.y, o.z, d.x, d.y, d.z, o.x, o.y, o.z, R(1), R(0.001), Num<R>::inf(), false, t)) {
+        V<R> ph = o + t * d;
+        add = thr * tex_sample(sc.texs[sc.background], ph);
+        has_add = true;
+      }
+    }
+    done = true;
+  } else {
+    uint32_t ty = etype(h.e), idx = epay(h.e);
+    V<R> pw, n;
+    bool front;
+    int32_t mat;
+    if (ty == E_VOLUME) {  // volumne.h:40-44
+      pw = o + h.t * d;
+      n = mkv(R(1), R(0), R(0));
+      front = true;
+      mat = sc.vols[idx].phase_mat;
+    } else {
+      V<R> oo = o, dd = d;
+      const Instance<R>* in = nullptr;
+      if (h.i >= 0) {
+        in = &sc.insts[h.i];
+        chain_in(*in, oo, dd);
+      }
+      V<R> po = oo + h.t * dd;
+      V<R> outward;
+      if (ty == E_QUAD) {
+        const Quad<R>& q = sc.quads[idx];
+        outward = ld3(q.n);
+        mat = q.mat;
+      } else if (ty == E_SPHERE) {  // sphere.h:69 (center_ member; (0,0,0) for moving spheres)
+        const Sphere<R>& s = sc.spheres[idx];
+        outward = (po - ld3(s.cn)) / s.r;
+        mat = s.mat;
+      } else {
+        const Tri<R>& tr = sc.tris[idx];
+        outward = ld3(tr.n);
+        mat = tr.mat;
+      }
+      front = dot(dd, outward) < R(0);  // hit_record::set_face_normal (hittable.h:26-29)
+      n = front ? outward : -outward;
+      pw = po;
+      if (in) {
+        for (int q = in->nops - 1; q >= 0; q--) {
+          pw = op_out(in->op[q], pw, true);
+          n = op_out(in->op[q], n, false);
+        }
+      }
+    }
+    const Material<R>& m = sc.mats[mat];
+    if (m.kind == M_DIFFUSE_LIGHT) {  // material.h:211-215; no scatter
+      if (front) {
+        add = thr * tex_sample(sc.texs[m.tex], pw);
+        has_add = true;
+      }
+      done = true;
+    } else {
+      V<R> att = tex_sample(sc.texs[m.tex], pw);
+      uint32_t js = 0;
+      auto U = [&]() { return to_unit<R>(draw_u32(k.ka, k.kb, dim_scatter(bounce, js++))); };
+      if (m.kind == M_METAL) {  // material.h:85-92
+        V<R> dir = unit(reflect(d, n));
+        R u1 = U();
+        R u2 = U();
+        new_d = dir + m.fuzz * unit(on_sphere(u1, u2));
+        thr = thr * att;
+      } else if (m.kind == M_DIELECTRIC) {  // material.h:113-131
+        R ri = front ? (R(1) / m.refr) : m.refr;
+        V<R> ud = unit(d);
+        R cos_t = fmin(dot(-ud, n), R(1));
+        R sin_t = sqrt(R(1) - cos_t * cos_t);
+        bool cant = ri * sin_t > R(1);
+        R r0 = (R(1) - ri) / (R(1) + ri);
+        r0 = r0 * r0;
+        if (cant || (r0 + (R(1) - r0) * pow(R(1) - cos_t, R(5))) > U())
+          new_d = reflect(ud, n);
+        else
+          new_d = refract(ud, n, ri);
+        thr = thr * att;
+      } else {  // lambertian (material.h:62-72) / isotropic (material.h:193-200): kRandom
+        const bool iso = m.kind == M_ISOTROPIC;
+        const R inv_pi = R(1) / Num<R>::pi();
+        const R iso_pdf = R(1) / (R(4) * Num<R>::pi());
+        Onb<R> b;
+        if (!iso) b = make_onb(n);
+        const Light<R>& L = *sc.light;
+        R pv;
+        V<R> dir;
+        if (L.kind == L_NONE) {  // camera.h:217-226
+          R u1 = U();
+          R u2 = U();
+          dir = iso ? unit(on_sphere(u1, u2)) : onb_transform(b, cosine_dir(u1, u2));
+          pv = iso ? iso_pdf : fmax(R(0), dot(unit(dir), b.y) / Num<R>::pi());
+        } else {  // dual_pdf(hittable_pdf(light), material pdf) (camera.h:227-239, pdf.h:48-61)
+          R c = U();
+          R u1 = U();
+          R u2 = U();
+          if (c < R(0.5))
+            dir = light_random(L, pw, u1, u2);
+          else
+            dir = iso ? unit(on_sphere(u1, u2)) : onb_transform(b, cosine_dir(u1, u2));
+          R mp = iso ? iso_pdf : fmax(R(0), dot(unit(dir), b.y) / Num<R>::pi());
+          pv = R(0.5) * light_pdf(L, pw, dir) + R(0.5) * mp;
+        }
+        R ps;
+        if (iso) {
+          ps = iso_pdf;
+        } else {
+          R c = dot(n, unit(dir));
+          ps = c < R(0) ? R(0) : c * inv_pi;
+        }
+        (void)inv_pi;
+        thr = thr * ((att * ps) / pv);
+        new_d = dir;
+      }
+      new_o = pw;
+      if ((int32_t)bounce + 1 >= p.max_depth) done = true;  // ray_color(.., 0) returns 0
+      if (thr.x == R(0) && thr.y == R(0) && thr.z == R(0)) done = true;
+    }
+  }
+
+  if (!done) {
+    if (has_add) {
+      R4<R> Lv = p.L[slot];
+      p.L[slot] = {Lv.x + add.x, Lv.y + add.y, Lv.z + add.z, R(0)};
+    }
+    p.O[slot] = {new_o.x, new_o.y, new_o.z, tm};
+    p.D[slot] = {new_d.x, new_d.y, new_d.z, R(bounce + 1)};
+    p.T[slot] = {thr.x, thr.y, thr.z, R(0)};
+    return;
+  }
+  // finish the sample (camera.h:167): add its radiance to the item's running sum
+  R4<R> Lv = p.L[slot];
+  R4<R> Av = p.A[slot];
+  V<R> rad = mkv(Lv.x, Lv.y, Lv.z);
+  if (has_add) rad = rad + add;
+  R4<R> acc{Av.x + rad.x, Av.y + rad.y, Av.z + rad.z, R(0)};
+  uint32_t item = S.z, sample = S.w + 1;
+  uint32_t chunk_end = min((item / p.npix) * p.chunk + p.chunk, p.spp);
+  if (sample >= chunk_end) {
+    R* dst = p.partial + 3ull * item;
+    dst[0] = acc.x;
+    dst[1] = acc.y;
+    dst[2] = acc.z;
+    acc = {R(0), R(0), R(0), R(0)};
+    item += p.P;
+    if (item >= p.n_items) {
+      p.D[slot] = {R(0), R(0), R(0), R(-1)};
+      return;
+    }
+    sample = (item / p.npix) * p.chunk;
+  }
+  begin_sample(p, slot, item, sample, acc);
+}
+
+// ------------------------------------------------------------------ live-slot compaction
+__device__ __forceinline__ bool slot_alive(const void* Dp, int prec, uint32_t slot) {
+  if (prec == RT_PREC_F32) return reinterpret_cast<const R4<float>*>(Dp)[slot].w >= 0.f;
+  return reinterpret_cast<const R4<double>*>(Dp)[slot].w >= 0.0;
+}
+
+__global__ __launch_bounds__(kBlock) void k_count(const void* Dp, int prec, const uint32_t* queue, uint32_t n,
+                                                  uint32_t* blk) {
+  __shared__ uint32_t wc[kBlock / 64];
+  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  bool alive = false;
+  if (i < n) alive = slot_alive(Dp, prec, queue ? queue[i] : i);
+  unsigned long long m = __ballot(alive);
+  if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = (uint32_t)__popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) blk[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
+}
+
+// exclusive scan of the per-block counts (one workgroup), total in *total
+__global__ __launch_bounds__(1024) void k_scan(uint32_t* blk, uint32_t nb, uint32_t* total) {
+  __shared__ uint32_t part[1024];
+  uint32_t per = (nb + 1023) / 1024;
+  uint32_t b = threadIdx.x * per, e = min(nb, b + per);
+  uint32_t s = 0;
+  for (uint32_t j = b; j < e; j++) s += blk[j];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (uint32_t off = 1; off < 1024; off <<= 1) {
+    uint32_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[threadIdx.x] - s;
+  for (uint32_t j = b; j < e; j++) {
+    uint32_t c = blk[j];
+    blk[j] = run;
+    run += c;
+  }
+  if (threadIdx.x == 1023) *total = part[1023];
+}
+
+__global__ __launch_bounds__(kBlock) void k_compact(const void* Dp, int prec, const uint32_t* queue, uint32_t n,
+                                                    const uint32_t* blk_off, uint32_t* out) {
+  __shared__ uint32_t wc[kBlock / 64];
+  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  uint32_t slot = 0;
+  bool alive = false;
+  if (i < n) {
+    slot = queue ? queue[i] : i;
+    alive = slot_alive(Dp, prec, slot);
+  }
+  unsigned long long m = __ballot(alive);
+  int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) wc[wave] = (uint32_t)__popcll(m);
+  __syncthreads();
+  uint32_t base = blk_off[blockIdx.x];
+  for (int w = 0; w < wave; w++) base += wc[w];
+  if (alive) {
+    unsigned long long below = lane ? (m & ((1ull << lane) - 1ull)) : 0ull;
+    out[base + (uint32_t)__popcll(below)] = slot;
+  }
+}
+
+// ------------------------------------------------------------------ resolve (camera.h:169-170)
+template <class R>
+__global__ __launch_bounds__(kBlock) void k_resolve(const R* partial, uint32_t npix, uint32_t nchunks, uint32_t spp,
+                                                    R* out) {
+  uint32_t px = blockIdx.x * kBlock + threadIdx.x;
+  if (px >= npix) return;
+  R s0 = 0, s1 = 0, s2 = 0;
+  for (uint32_t c = 0; c < nchunks; c++) {
+    const R* q = partial + 3ull * ((uint64_t)c * npix + px);
+    s0 += q[0];
+    s1 += q[1];
+    s2 += q[2];
+  }
+  R inv = R(spp);
+  out[3ull * px] = s0 / inv;
+  out[3ull * px + 1] = s1 / inv;
+  out[3ull * px + 2] = s2 / inv;
+}
+
+template <class R>
+__global__ void k_zero(R* out, uint64_t n) {
+  uint64_t i = blockIdx.x * (uint64_t)kBlock + threadIdx.x;
+  if (i < n) out[i] = R(0);
+}
+
+// camera.h:137-141 and 246 evaluated in double exactly as the reference orders them
+struct View {
+  double du[3], dv[3], dir00[3], pos[3];
+};
+View make_view(const rt_camera_desc* c) {
+  View v;
+  for (int k = 0; k < 3; k++) {
+    v.du[k] = (c->right[k] * c->viewport_width) / (double)c->image_width;
+    v.dv[k] = (c->up[k] * -c->viewport_height) / (double)c->image_height;
+  }
+  for (int k = 0; k < 3; k++) {
+    double a = c->dir[k] * c->focal_length;
+    double b = c->right[k] * (c->viewport_width / 2.0);
+    double u = c->up[k] * (c->viewport_height / 2.0);
+    double e = (v.du[k] + v.dv[k]) * 0.5;
+    v.dir00[k] = ((a - b) + u) + e;
+    v.pos[k] = c->pos[k];
+  }
+  return v;
+}
+
+template <class R>
+V<R> tov(const double* a) {
+  return {(R)a[0], (R)a[1], (R)a[2]};
+}
+
+}  // namespace
+
+// ====================================================================== host side
+
+struct DevBuf {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+};
+
+struct rt_context {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  CompiledScene scene;
+  bool has_scene = false;
+  DevBuf scene32, scene64;
+  DevBuf state, partial, pixmap, queue0, queue1, blk, out_tmp, counters;
+  uint32_t* total_host = nullptr;  // pinned
+  uint64_t samples = 0;
+  rt_counters last{};
+  int timing = 0;
+  std::vector<hipEvent_t> events;
+};
+
+namespace {
+
+std::mutex g_err_mu;
+std::string g_create_err;
+
+rt_status set_err(rt_context* c, rt_status s, const std::string& m) {
+  if (c) {
+    c->err = m;
+  } else {
+    std::lock_guard<std::mutex> lk(g_err_mu);
+    g_create_err = m;
+  }
+  return s;
+}
+
+#define RT_HIP(ctx, call)                                                                   \
+  do {                                                                                      \
+    hipError_t e_ = (call);                                                                 \
+    if (e_ != hipSuccess)                                                                   \
+      return set_err((ctx), RT_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+rt_status ensure(rt_context* c, DevBuf& b, size_t bytes) {
+  if (b.ptr && b.bytes >= bytes) return RT_OK;
+  if (b.ptr) {
+    RT_HIP(c, hipDeviceSynchronize());
+    RT_HIP(c, hipFree(b.ptr));
+    b.ptr = nullptr;
+    b.bytes = 0;
+  }
+  size_t want = std::max<size_t>(bytes, 256);
+  hipError_t e = hipMalloc(&b.ptr, want);
+  if (e != hipSuccess) {
+    b.ptr = nullptr;
+    (void)hipGetLastError();
+    return set_err(c, RT_ERR_OUT_OF_MEMORY,
+                   "hipMalloc(" + std::to_string(want) + " bytes): " + hipGetErrorString(e));
+  }
+  b.bytes = want;
+  return RT_OK;
+}
+
+hipEvent_t take_event(rt_context* c, size_t idx) {
+  while (c->events.size() <= idx) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    c->events.push_back(e);
+  }
+  return c->events[idx];
+}
+
+template <class R>
+DevScene<R> dev_scene(const SceneHeader& h, void* base) {
+  auto at = [&](uint64_t off) { return (const unsigned char*)base + off; };
+  DevScene<R> s{};
+  s.quads = (const Quad<R>*)at(h.off_quads);
+  s.spheres = (const Sphere<R>*)at(h.off_spheres);
+  s.tris = (const Tri<R>*)at(h.off_tris);
+  s.insts = (const Instance<R>*)at(h.off_instances);
+  s.vols = (const Volume<R>*)at(h.off_volumes);
+  s.nodes = (const Node<R>*)at(h.off_nodes);
+  s.refs = (const uint32_t*)at(h.off_refs);
+  s.mats = (const Material<R>*)at(h.off_mats);
+  s.texs = (const Texture<R>*)at(h.off_texs);
+  s.light = (const Light<R>*)at(h.off_light);
+  s.root = h.root;
+  s.background = h.background;
+  s.has_volumes = h.has_volumes;
+  return s;
+}
+
+template <class R>
+void launch_extend2(const Params<R>& p, int stack, uint32_t grid, hipStream_t st) {
+  if (stack <= 8)
+    hipLaunchKernelGGL((k_extend<R, 8>), dim3(grid), dim3(kBlock), 0, st, p);
+  else if (stack <= 16)
+    hipLaunchKernelGGL((k_extend<R, 16>), dim3(grid), dim3(kBlock), 0, st, p);
+  else
+    hipLaunchKernelGGL((k_extend<R, kStackDepth>), dim3(grid), dim3(kBlock), 0, st, p);
+}
+
+template <class R>
+rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_params* prm, const rt_tile* tiles,
+                 int32_t ntiles, void* out, int32_t out_dev, hipStream_t st) {
+  const bool f64 = sizeof(R) == 8;
+  const CompiledScene& cs = c->scene;
+  const SceneHeader& hdr = f64 ? cs.hdr64 : cs.hdr;
+  void* sbase = f64 ? c->scene64.ptr : c->scene32.ptr;
+  auto t0 = std::chrono::steady_clock::now();
+  rt_counters last{};
+
+  // pixel map: tiles packed in order, row-major inside each tile
+  std::vector<uint32_t> pix;
+  for (int t = 0; t < ntiles; t++)
+    for (int y = 0; y < tiles[t].height; y++)
+      for (int x = 0; x < tiles[t].width; x++)
+        pix.push_back((uint32_t)(tiles[t].y0 + y) * (uint32_t)cam->image_width + (uint32_t)(tiles[t].x0 + x));
+  const uint32_t npix = (uint32_t)pix.size();
+  if (npix == 0) return RT_OK;
+  const size_t out_elems = 3ull * npix;
+  rt_status s;
+  void* dout = out;
+  if (!out_dev) {
+    if ((s = ensure(c, c->out_tmp, out_elems * sizeof(R))) != RT_OK) return s;
+    dout = c->out_tmp.ptr;
+  }
+
+  if (prm->max_depth <= 0) {  // ray_color(r, 0) is black for every sample (camera.h:194-195)
+    hipLaunchKernelGGL(k_zero<R>, dim3((unsigned)((out_elems + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                       (R*)dout, (uint64_t)out_elems);
+  } else {
+    const uint32_t spp = (uint32_t)prm->spp;
+    const uint32_t chunk = prm->samples_per_item > 0 ? std::min<uint32_t>((uint32_t)prm->samples_per_item, spp)
+                                                     : std::min<uint32_t>(kAutoChunk, spp);
+    const uint32_t nchunks = (spp + chunk - 1) / chunk;
+    const uint64_t n_items64 = (uint64_t)npix * nchunks;
+    if (n_items64 >= (1ull << 31)) return set_err(c, RT_ERR_INVALID_ARGUMENT, "too many work items in one call");
+    const uint32_t n_items = (uint32_t)n_items64;
+    uint32_t P = prm->pool_slots > 0 ? (uint32_t)prm->pool_slots : (f64 ? kAutoPool64 : kAutoPool32);
+    P = std::max<uint32_t>(1, std::min(P, n_items));
+    const uint32_t nblk_max = (P + kBlock - 1) / kBlock;
+
+    // path state: 5 R4 arrays + hit records + uint4 keys, each P long
+    auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+    const size_t r4 = al(sizeof(R4<R>) * (size_t)P), hb = al(sizeof(HitRec<R>) * (size_t)P), sb = al(16 * (size_t)P);
+    if ((s = ensure(c, c->state, 5 * r4 + hb + sb)) != RT_OK) return s;
+    if ((s = ensure(c, c->partial, 3ull * n_items * sizeof(R))) != RT_OK) return s;
+    if ((s = ensure(c, c->pixmap, 4ull * npix)) != RT_OK) return s;
+    if ((s = ensure(c, c->queue0, 4ull * P)) != RT_OK) return s;
+    if ((s = ensure(c, c->queue1, 4ull * P)) != RT_OK) return s;
+    if ((s = ensure(c, c->blk, 4ull * (nblk_max + 2))) != RT_OK) return s;
+    RT_HIP(c, hipMemcpyAsync(c->pixmap.ptr, pix.data(), 4ull * npix, hipMemcpyHostToDevice, st));
+    RT_HIP(c, hipMemsetAsync(c->counters.ptr, 0, sizeof(unsigned long long) * kSegShards, st));
+
+    unsigned char* sp = (unsigned char*)c->state.ptr;
+    Params<R> p{};
+    p.sc = dev_scene<R>(hdr, sbase);
+    p.O = (R4<R>*)sp;
+    p.D = (R4<R>*)(sp + r4);
+    p.T = (R4<R>*)(sp + 2 * r4);
+    p.L = (R4<R>*)(sp + 3 * r4);
+    p.A = (R4<R>*)(sp + 4 * r4);
+    p.H = (HitRec<R>*)(sp + 5 * r4);
+    p.S = (uint4*)(sp + 5 * r4 + hb);
+    p.partial = (R*)c->partial.ptr;
+    p.pixmap = (const uint32_t*)c->pixmap.ptr;
+    p.queue = nullptr;
+    p.n = P;
+    p.P = P;
+    p.npix = npix;
+    p.n_items = n_items;
+    p.chunk = chunk;
+    p.spp = spp;
+    p.first_sample = (uint32_t)std::max(0, prm->first_sample);
+    p.W = (uint32_t)cam->image_width;
+    p.max_depth = prm->max_depth;
+    p.seed = prm->seed;
+    View vw = make_view(cam);
+    p.pos = tov<R>(vw.pos);
+    p.du = tov<R>(vw.du);
+    p.dv = tov<R>(vw.dv);
+    p.dir00 = tov<R>(vw.dir00);
+    p.seg_shards = (unsigned long long*)c->counters.ptr;
+
+    hipLaunchKernelGGL(k_init<R>, dim3(nblk_max), dim3(kBlock), 0, st, p);
+    uint64_t launches = 1, iters = 0;
+    uint32_t* qbuf[2] = {(uint32_t*)c->queue0.ptr, (uint32_t*)c->queue1.ptr};
+    int qsel = 0;
+    uint32_t* blk = (uint32_t*)c->blk.ptr;
+    uint32_t* d_total = blk + nblk_max + 1;
+    size_t ev = 0;
+    std::vector<std::pair<int, size_t>> timed;  // (0 extend / 1 shade, event index)
+    // every slot finishes within (items per slot) * chunk * max_depth rounds; anything longer is a bug
+    const uint64_t iter_cap = ((uint64_t)(n_items + P - 1) / P) * chunk * (uint64_t)prm->max_depth + 4 * kBatch;
+    for (;;) {
+      if (iters > iter_cap) return set_err(c, RT_ERR_HIP, "wavefront did not drain (internal error)");
+      const uint32_t grid = (p.n + kBlock - 1) / kBlock;
+      for (int b = 0; b < kBatch; b++) {
+        hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
+        if (c->timing) {
+          e0 = take_event(c, ev);
+          e1 = take_event(c, ev + 1);
+          e2 = take_event(c, ev + 2);
+          if (!e0 || !e1 || !e2) return set_err(c, RT_ERR_HIP, "hipEventCreate failed");
+          RT_HIP(c, hipEventRecord(e0, st));
+        }
+        launch_extend2<R>(p, cs.stack_need, grid, st);
+        if (c->timing) RT_HIP(c, hipEventRecord(e1, st));
+        hipLaunchKernelGGL(k_shade<R>, dim3(grid), dim3(kBlock), 0, st, p);
+        if (c->timing) {
+          RT_HIP(c, hipEventRecord(e2, st));
+          timed.push_back({0, ev});
+          ev += 3;
+        }
+        launches += 2;
+        iters++;
+      }
+      RT_HIP(c, hipGetLastError());
+      // live-slot count; compact into a queue once half the pool has finished
+      hipLaunchKernelGGL(k_count, dim3(grid), dim3(kBlock), 0, st, (const void*)p.D, (int)f64, p.queue, p.n, blk);
+      hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, blk, grid, d_total);
+      launches += 2;
+      RT_HIP(c, hipMemcpyAsync(c->total_host, d_total, 4, hipMemcpyDeviceToHost, st));
+      RT_HIP(c, hipStreamSynchronize(st));
+      uint32_t alive = *c->total_host;
+      if (alive == 0) break;
+      if (p.queue || alive * 2 <= p.P) {
+        uint32_t* nq = qbuf[qsel];
+        qsel ^= 1;
+        hipLaunchKernelGGL(k_compact, dim3(grid), dim3(kBlock), 0, st, (const void*)p.D, (int)f64, p.queue, p.n,
+                           (const uint32_t*)blk, nq);
+        launches++;
+        p.queue = nq;
+        p.n = alive;
+      }
+    }
+    hipLaunchKernelGGL(k_resolve<R>, dim3((npix + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
+                       (const R*)c->partial.ptr, npix, nchunks, spp, (R*)dout);
+    launches++;
+    RT_HIP(c, hipGetLastError());
+    // counters
+    unsigned long long shards[kSegShards];
+    RT_HIP(c, hipMemcpyAsync(shards, c->counters.ptr, sizeof shards, hipMemcpyDeviceToHost, st));
+    RT_HIP(c, hipStreamSynchronize(st));
+    uint64_t segs = 0;
+    for (int k = 0; k < kSegShards; k++) segs += shards[k];
+    last.segments = segs;
+    last.samples = (uint64_t)npix * spp;
+    last.iterations = iters;
+    last.launches = launches;
+    if (c->timing) {
+      double ext = 0, sh = 0;
+      for (auto& t : timed) {
+        float a = 0, b = 0;
+        RT_HIP(c, hipEventElapsedTime(&a, c->events[t.second], c->events[t.second + 1]));
+        RT_HIP(c, hipEventElapsedTime(&b, c->events[t.second + 1], c->events[t.second + 2]));
+        ext += a;
+        sh += b;
+      }
+      last.extend_ms = ext;
+      last.shade_ms = sh;
+    }
+  }
+  if (!out_dev) {
+    RT_HIP(c, hipMemcpyAsync(out, dout, out_elems * sizeof(R), hipMemcpyDeviceToHost, st));
+  }
+  RT_HIP(c, hipStreamSynchronize(st));
+  last.last_render_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  uint64_t seg_total = c->last.segments + last.segments, smp_total = c->last.samples + last.samples;
+  c->last = last;
+  c->last.segments = seg_total;  // cumulative since rt_reset_counters
+  c->last.samples = smp_total;
+  return RT_OK;
+}
+
+}  // namespace
+
+// ====================================================================== C ABI
+
+extern "C" {
+
+int32_t rt_abi_version(void) { return RT_ABI_VERSION; }
+
+rt_status rt_context_create(int32_t device, rt_context** out) {
+  if (!out) return set_err(nullptr, RT_ERR_INVALID_ARGUMENT, "out is null");
+  *out = nullptr;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0) {
+    (void)hipGetLastError();
+    return set_err(nullptr, RT_ERR_NO_DEVICE, std::string("no HIP device: ") + hipGetErrorString(e));
+  }
+  if (device < 0 || device >= n) return set_err(nullptr, RT_ERR_INVALID_ARGUMENT, "device index out of range");
+  if ((e = hipSetDevice(device)) != hipSuccess) return set_err(nullptr, RT_ERR_HIP, hipGetErrorString(e));
+  auto* c = new rt_context;
+  c->device = device;
+  if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
+    delete c;
+    return set_err(nullptr, RT_ERR_HIP, hipGetErrorString(e));
+  }
+  if ((e = hipHostMalloc((void**)&c->total_host, 64, hipHostMallocDefault)) != hipSuccess) {
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return set_err(nullptr, RT_ERR_HIP, hipGetErrorString(e));
+  }
+  if (ensure(c, c->counters, sizeof(unsigned long long) * kSegShards) != RT_OK) {
+    std::string m = c->err;
+    rt_context_destroy(c);
+    return set_err(nullptr, RT_ERR_OUT_OF_MEMORY, m);
+  }
+  *out = c;
+  return RT_OK;
+}
+
+void rt_context_destroy(rt_context* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (DevBuf* b : {&c->scene32, &c->scene64, &c->state, &c->partial, &c->pixmap, &c->queue0, &c->queue1, &c->blk,
+                    &c->out_tmp, &c->counters})
+    if (b->ptr) (void)hipFree(b->ptr);
+  for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
+  if (c->total_host) (void)hipHostFree(c->total_host);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* rt_last_error(const rt_context* c) {
+  if (c) return c->err.c_str();
+  std::lock_guard<std::mutex> lk(g_err_mu);
+  return g_create_err.c_str();
+}
+
+rt_status rt_scene_upload(rt_context* c, const rt_scene_desc* desc) {
+  if (!c || !desc) return set_err(c, RT_ERR_INVALID_ARGUMENT, "null context or descriptor");
+  RT_HIP(c, hipSetDevice(c->device));
+  CompiledScene cs;
+  std::string err;
+  rt_status s = compile_scene(desc, &cs, &err);
+  if (s != RT_OK) return set_err(c, s, err);
+  if ((s = ensure(c, c->scene32, cs.blob32.size())) != RT_OK) return s;
+  if ((s = ensure(c, c->scene64, cs.blob64.size())) != RT_OK) return s;
+  RT_HIP(c, hipMemcpyAsync(c->scene32.ptr, cs.blob32.data(), cs.blob32.size(), hipMemcpyHostToDevice, c->stream));
+  RT_HIP(c, hipMemcpyAsync(c->scene64.ptr, cs.blob64.data(), cs.blob64.size(), hipMemcpyHostToDevice, c->stream));
+  RT_HIP(c, hipStreamSynchronize(c->stream));
+  c->scene = std::move(cs);
+  c->has_scene = true;
+  return RT_OK;
+}
+
+rt_status rt_render_tiles(rt_context* c, const rt_camera_desc* cam, const rt_render_params* prm, const rt_tile* tiles,
+                          int32_t ntiles, void* out_rgb, int32_t out_is_device, void* stream) {
+  if (!c) return set_err(nullptr, RT_ERR_INVALID_ARGUMENT, "null context");
+  if (!cam || !prm || (!tiles && ntiles > 0) || ntiles < 0 || (!out_rgb && ntiles > 0))
+    return set_err(c, RT_ERR_INVALID_ARGUMENT, "null argument");
+  if (!c->has_scene) return set_err(c, RT_ERR_NO_SCENE, "rt_scene_upload has not succeeded on this context");
+  if (cam->mode != RT_CAM_PERSPECTIVE)
+    return set_err(c, RT_ERR_UNSUPPORTED, "only the perspective camera (camera.h:245-251) runs on the device");
+  if (cam->image_width <= 0 || cam->image_height <= 0) return set_err(c, RT_ERR_INVALID_ARGUMENT, "empty image");
+  if (prm->spp <= 0) return set_err(c, RT_ERR_INVALID_ARGUMENT, "spp must be positive");
+  if (prm->precision != RT_PREC_F32 && prm->precision != RT_PREC_F64)
+    return set_err(c, RT_ERR_INVALID_ARGUMENT, "unknown precision");
+  for (int t = 0; t < ntiles; t++) {
+    const rt_tile& tl = tiles[t];
+    if (tl.x0 < 0 || tl.y0 < 0 || tl.width < 0 || tl.height < 0 || tl.x0 + tl.width > cam->image_width ||
+        tl.y0 + tl.height > cam->image_height)
+      return set_err(c, RT_ERR_INVALID_ARGUMENT, "tile " + std::to_string(t) + " outside the image");
+  }
+  RT_HIP(c, hipSetDevice(c->device));
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  if (prm->precision == RT_PREC_F64) return render<double>(c, cam, prm, tiles, ntiles, out_rgb, out_is_device, st);
+  return render<float>(c, cam, prm, tiles, ntiles, out_rgb, out_is_device, st);
+}
+
+rt_status rt_stats(rt_context* c, rt_counters* out) {
+  if (!c || !out) return set_err(c, RT_ERR_INVALID_ARGUMENT, "null argument");
+  *out = c->last;
+  return RT_OK;
+}
+
+rt_status rt_reset_counters(rt_context* c) {
+  if (!c) return set_err(nullptr, RT_ERR_INVALID_ARGUMENT, "null context");
+  c->last = rt_counters{};
+  return RT_OK;
+}
+
+rt_status rt_set_timing(rt_context* c, int32_t enable) {
+  if (!c) return set_err(nullptr, RT_ERR_INVALID_ARGUMENT, "null context");
+  c->timing = enable ? 1 : 0;
+  return RT_OK;
+}
+
+uint32_t rt_rng_u32(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t dim) {
+  return draw_u32(key_pixel(seed, pixel), key_sample(seed, sample), dim);
+}
+
+}  // extern "C"

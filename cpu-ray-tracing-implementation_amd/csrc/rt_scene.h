@@ -1,0 +1,168 @@
+// rt_scene.h -- device scene layout (shared by the host scene compiler and the
+// HIP kernels). Everything is a flat array; records are 16-byte aligned so a
+// lane fetches a record with dwordx4 loads.
+//
+// The hittable DAG of the reference (hittable.h, hittable_list.h, bvh_node.h,
+// sphere.h, quad.h, triangle.h, volumne.h) is compiled into a stack machine:
+// every traversal step pops a 32-bit *entry* whose top 3 bits say what it is.
+//
+//   QUAD / SPHERE / TRI (i)  a primitive, tested inline where it appears in a list
+//   INSTANCE (i)             translate/rotate_* wrappers (hittable.h:67-293): the
+//                            ray is re-derived from the world ray through the
+//                            instance's transform chain, then its BLAS entry runs
+//   VOLUME (i)               volumne::hit (volumne.h:18-46), tested inline
+//   NODE (i)                 BVH node: two child boxes, children are entries
+//   LIST (pos)               refs[pos], refs[pos+1], ... until END, in order --
+//                            hittable_list::hit semantics (closest, later wins ties)
+//   SPECIAL: END (in refs), RESTORE(k) (on the stack: back to instance k-1 / world)
+#pragma once
+
+#include <stdint.h>
+
+namespace rtd {
+
+enum : uint32_t {
+  E_QUAD = 0u,
+  E_SPHERE = 1u,
+  E_TRI = 2u,
+  E_INSTANCE = 3u,
+  E_VOLUME = 4u,
+  E_NODE = 5u,
+  E_LIST = 6u,
+  E_SPECIAL = 7u,
+};
+constexpr uint32_t kTypeShift = 29;
+constexpr uint32_t kPayloadMask = (1u << kTypeShift) - 1u;
+constexpr uint32_t kEnd = (E_SPECIAL << kTypeShift) | 0u;
+constexpr uint32_t kRestoreBase = (E_SPECIAL << kTypeShift) | 1u;  // RESTORE(k) = kRestoreBase + k
+constexpr uint32_t kNoHit = 0xFFFFFFFFu;
+
+__host__ __device__ inline uint32_t etype(uint32_t e) { return e >> kTypeShift; }
+__host__ __device__ inline uint32_t epay(uint32_t e) { return e & kPayloadMask; }
+__host__ __device__ inline uint32_t mk(uint32_t type, uint32_t payload) { return (type << kTypeShift) | payload; }
+
+constexpr int kMaxChain = 4;    // translate/rotate wrappers per instance (composed, outermost first)
+constexpr int kStackDepth = 32;  // traversal stack entries per lane (LDS)
+constexpr int kMaxBvhDepth = 26; // the builder keeps every BVH within this depth
+
+// quad.h:9-23 precomputed: n = unit(cross(u,v)), D = dot(n, corner),
+// a = cross(v, w), b = cross(w, u) with w = cross(u,v)/dot(cross(u,v),cross(u,v)),
+// so alpha = dot(p - corner, a) = dot(w, cross(p - corner, v)) and beta = dot(p - corner, b).
+template <class R>
+struct alignas(16) Quad {
+  R n[3];
+  R D;
+  R q[3];
+  int32_t mat;
+  R a[3];
+  R area;
+  R b[3];
+  R pad;
+};
+
+// sphere.h:7-35. c1 = center (static) / center1 (moving); dc = center2 - center1;
+// cn = the `center_` member used for the normal (sphere.h:69): c1 for the static
+// constructors, (0,0,0) for the moving one, as in the reference.
+template <class R>
+struct alignas(16) Sphere {
+  R c1[3];
+  R r;
+  R dc[3];
+  int32_t mat;
+  R cn[3];
+  int32_t moving;
+};
+
+// triangle.h:8-40: e1 = p1 - p0, e2 = p2 - p0, n = unit(cross(e1, e2)).
+template <class R>
+struct alignas(16) Tri {
+  R p0[3];
+  int32_t mat;
+  R e1[3];
+  R pad1;
+  R e2[3];
+  R pad2;
+  R n[3];
+  R pad3;
+};
+
+// One wrapper of a chain, applied world -> object in order (hittable.h:75-82, 125-149, ...).
+// kind 0: translate by (x, y, z); kind 1/2/3: rotate about x/y/z with (s, c).
+template <class R>
+struct alignas(16) XOp {
+  R x, y, z;
+  int32_t kind;
+};
+
+template <class R>
+struct alignas(16) Instance {
+  XOp<R> op[kMaxChain];
+  int32_t nops;
+  uint32_t blas;  // entry of the wrapped hittable (object space)
+  int32_t pad[2];
+};
+
+// volumne.h:9-46: boundary = refs list at `boundary` (object space of chain `inst`,
+// -1 = world). neg_inv_density = -1.0 / density (volumne.h:36).
+template <class R>
+struct alignas(16) Volume {
+  R neg_inv_density;
+  int32_t inst;
+  uint32_t boundary;  // LIST entry of the boundary primitives
+  int32_t phase_mat;
+};
+
+template <class R>
+struct alignas(16) Node {
+  R lo[2][3];
+  R hi[2][3];
+  uint32_t child[2];
+};
+
+enum : int32_t { M_LAMBERTIAN = 1, M_METAL = 2, M_DIELECTRIC = 3, M_ISOTROPIC = 4, M_DIFFUSE_LIGHT = 5 };
+enum : int32_t { T_SOLID = 1, T_CHECKER = 2 };
+
+template <class R>
+struct alignas(16) Material {
+  int32_t kind;
+  int32_t tex;
+  R fuzz;  // float in the reference (material.h:96); widened exactly
+  R refr;  // float in the reference (material.h:142)
+};
+
+template <class R>
+struct alignas(16) Texture {
+  R c0[3];  // solid color / checker odd
+  int32_t kind;
+  R c1[3];  // checker even
+  R scale;  // checker (texture.h:48)
+};
+
+// The importance-sampling light (camera.h:135 `light`, hittable_list.h:39-50).
+enum : int32_t { L_NONE = 0, L_BASE = 1, L_QUAD = 2, L_SPHERE = 3 };
+template <class R>
+struct alignas(16) Light {
+  int32_t kind;
+  int32_t pad[3];
+  Quad<R> quad;  // L_QUAD (quad.h:66-78)
+  R u[3];
+  R pad1;
+  R v[3];
+  R pad2;
+  R center[3];  // L_SPHERE: center_ (sphere.h:76-81)
+  R radius;
+};
+
+// What the host uploads: offsets into one contiguous device blob.
+struct SceneHeader {
+  uint32_t root;      // entry of the world
+  int32_t background; // texture index or -1
+  int32_t has_volumes;
+  int32_t num_instances;
+  uint64_t off_quads, off_spheres, off_tris, off_instances, off_volumes, off_nodes, off_refs, off_mats, off_texs,
+      off_light;
+  uint64_t bytes;
+  uint32_t n_quads, n_spheres, n_tris, n_volumes, n_nodes, n_refs, n_mats, n_texs;
+};
+
+}  // namespace rtd

@@ -1,0 +1,737 @@
+// scene_compile.cpp -- hittable DAG -> device scene (see rt_scene.h).
+//
+// Semantics kept from the reference:
+//  * hittable_list::hit (hittable_list.h:20-31) is an ordered scan where the
+//    closest hit wins and, on equal t, the later object wins. Lists that hold a
+//    volume (whose hit draws a random number, volumne.h:36) or that are small
+//    stay ordered lists; larger volume-free lists and every bvh_node become a
+//    SAH BVH of our own (closest hit is independent of the tree except for
+//    exact-t ties).
+//  * translate / rotate_x/y/z (hittable.h:67-293) become instances holding the
+//    whole chain of wrappers from the world down to the object, applied in the
+//    reference's order and arithmetic, so object-space hits are bit-identical
+//    to the reference's nested calls in the fp64 path.
+//  * volumne (volumne.h:9-46) keeps its boundary as an ordered primitive list
+//    plus that boundary's wrapper chain.
+#include "scene_compile.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+
+namespace rtd {
+namespace {
+
+constexpr double kInf = std::numeric_limits<double>::infinity();
+constexpr int kSmallList = 8;  // lists up to this size stay ordered lists
+constexpr int kLeafMax = 4;
+
+struct Box {
+  double lo[3] = {kInf, kInf, kInf};
+  double hi[3] = {-kInf, -kInf, -kInf};
+  void grow(const double* p) {
+    for (int k = 0; k < 3; k++) {
+      lo[k] = std::min(lo[k], p[k]);
+      hi[k] = std::max(hi[k], p[k]);
+    }
+  }
+  void grow(const Box& b) {
+    for (int k = 0; k < 3; k++) {
+      lo[k] = std::min(lo[k], b.lo[k]);
+      hi[k] = std::max(hi[k], b.hi[k]);
+    }
+  }
+  bool empty() const { return !(lo[0] <= hi[0] && lo[1] <= hi[1] && lo[2] <= hi[2]); }
+  double area() const {
+    if (empty()) return 0;
+    double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    return 2 * (dx * dy + dy * dz + dz * dx);
+  }
+  double center(int k) const { return 0.5 * (lo[k] + hi[k]); }
+};
+
+struct Op {  // one wrapper, world -> object direction
+  int kind;  // 0 translate, 1/2/3 rotate x/y/z
+  double x, y, z;  // translate: offset; rotate: x = sin, y = cos
+};
+
+// object -> parent for a point (inverse of one Op), the reference's back-transform
+void op_to_parent(const Op& op, double p[3]) {
+  if (op.kind == 0) {
+    p[0] += op.x;
+    p[1] += op.y;
+    p[2] += op.z;
+    return;
+  }
+  int a = op.kind == 1 ? 1 : 0, b = op.kind == 3 ? 1 : 2;
+  double s = op.x, c = op.y;
+  double pa = p[a], pb = p[b];
+  p[a] = c * pa + s * pb;
+  p[b] = -s * pa + c * pb;
+}
+
+Box box_to_parent(const Box& in, const std::vector<Op>& ops) {  // ops outermost first
+  if (in.empty()) return in;
+  Box out;
+  for (int i = 0; i < 8; i++) {
+    double p[3] = {(i & 1) ? in.hi[0] : in.lo[0], (i & 2) ? in.hi[1] : in.lo[1], (i & 4) ? in.hi[2] : in.lo[2]};
+    for (int k = (int)ops.size() - 1; k >= 0; k--) op_to_parent(ops[(size_t)k], p);
+    out.grow(p);
+  }
+  // rotations are applied in double: widen by a relative margin so the box stays conservative
+  for (int k = 0; k < 3; k++) {
+    double m = 1e-9 * (std::fabs(out.lo[k]) + std::fabs(out.hi[k])) + 1e-12;
+    out.lo[k] -= m;
+    out.hi[k] += m;
+  }
+  return out;
+}
+
+inline void v_sub(const double* a, const double* b, double* o) {
+  for (int k = 0; k < 3; k++) o[k] = a[k] - b[k];
+}
+inline void v_cross(const double* a, const double* b, double* o) {  // vec3.h:79-82
+  double r0 = a[1] * b[2] - a[2] * b[1], r1 = a[2] * b[0] - a[0] * b[2], r2 = a[0] * b[1] - a[1] * b[0];
+  o[0] = r0;
+  o[1] = r1;
+  o[2] = r2;
+}
+inline double v_dot(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+inline void v_unit(const double* a, double* o) {  // vec3.h:77: v / v.length()
+  double l = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+  for (int k = 0; k < 3; k++) o[k] = a[k] / l;
+}
+
+struct Item {
+  uint32_t entry;
+  Box box;
+  int need;   // traversal stack entries processing this entry can add
+  int depth;  // BVH depth below this entry
+  bool volume;
+};
+
+class Compiler {
+ public:
+  explicit Compiler(const rt_scene_desc* d) : d_(d) {}
+
+  bool run(CompiledScene* out, std::string* err);
+
+ private:
+  const rt_scene_desc* d_;
+  std::string err_;
+  bool ok_ = true;
+
+  std::vector<Quad<double>> quads_;
+  std::vector<Sphere<double>> spheres_;
+  std::vector<Tri<double>> tris_;
+  std::vector<Instance<double>> insts_;
+  std::vector<Volume<double>> vols_;
+  std::vector<Node<double>> nodes_;
+  std::vector<uint32_t> refs_;
+  std::vector<Material<double>> mats_;
+  std::vector<Texture<double>> texs_;
+  Light<double> light_{};
+  int depth_guard_ = 0;
+
+  bool fail(const std::string& m) {
+    if (ok_) err_ = m;
+    ok_ = false;
+    return false;
+  }
+  const rt_object* obj(int i) {
+    if (i < 0 || i >= d_->num_objects) {
+      fail("object index " + std::to_string(i) + " out of range");
+      return nullptr;
+    }
+    return &d_->objects[i];
+  }
+  bool check_mat(int m) {
+    if (m < 0 || m >= d_->num_materials) return fail("primitive without a valid material");
+    return true;
+  }
+  static bool is_wrapper(int kind) { return kind >= RT_OBJ_TRANSLATE && kind <= RT_OBJ_ROTATE_Z; }
+  static Op op_of(const rt_object& o) {
+    if (o.kind == RT_OBJ_TRANSLATE) return {0, o.a[0], o.a[1], o.a[2]};
+    return {o.kind - RT_OBJ_ROTATE_X + 1, o.s0, o.s1, 0.0};
+  }
+
+  Item prim_item(const rt_object& o);
+  void gather(int idx, const std::vector<Op>& chain, std::vector<Item>& out, bool ordered_ctx);
+  Item container(std::vector<Item>& items, bool ordered);
+  Item list_of(const std::vector<Item>& items);
+  Item bvh(std::vector<Item>& items, size_t b, size_t e, int depth);
+  int make_instance(const std::vector<Op>& chain, uint32_t blas);
+  void light_from(int idx);
+};
+
+Item Compiler::prim_item(const rt_object& o) {
+  Item it{};
+  it.need = 0;
+  it.depth = 0;
+  it.volume = false;
+  if (!check_mat(o.material)) return it;
+  if (o.kind == RT_OBJ_QUAD) {  // quad.h:9-23
+    Quad<double> q{};
+    double n[3], nn;
+    v_cross(o.b, o.c, n);
+    v_unit(n, q.n);
+    q.area = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+    for (int k = 0; k < 3; k++) q.q[k] = o.a[k];
+    q.D = v_dot(q.n, q.q);
+    nn = v_dot(n, n);
+    double w[3] = {n[0] / nn, n[1] / nn, n[2] / nn};
+    v_cross(o.c, w, q.a);  // alpha = dot(w, cross(p, v)) = dot(p, cross(v, w))
+    v_cross(w, o.b, q.b);  // beta  = dot(w, cross(u, p)) = dot(p, cross(w, u))
+    q.mat = o.material;
+    quads_.push_back(q);
+    it.entry = mk(E_QUAD, (uint32_t)quads_.size() - 1);
+    double c1[3], c2[3], c3[3];
+    for (int k = 0; k < 3; k++) {
+      c1[k] = o.a[k] + o.b[k];
+      c2[k] = o.a[k] + o.c[k];
+      c3[k] = o.a[k] + o.b[k] + o.c[k];
+    }
+    it.box.grow(o.a);
+    it.box.grow(c1);
+    it.box.grow(c2);
+    it.box.grow(c3);
+  } else if (o.kind == RT_OBJ_SPHERE) {  // sphere.h:7-35
+    Sphere<double> s{};
+    double r = std::fmax(0, o.s0);
+    for (int k = 0; k < 3; k++) {
+      s.c1[k] = o.a[k];
+      s.dc[k] = o.moving ? (o.b[k] - o.a[k]) : 0.0;
+      s.cn[k] = o.moving ? 0.0 : o.a[k];
+    }
+    s.r = r;
+    s.mat = o.material;
+    s.moving = o.moving ? 1 : 0;
+    spheres_.push_back(s);
+    it.entry = mk(E_SPHERE, (uint32_t)spheres_.size() - 1);
+    double lo[3], hi[3];
+    for (int k = 0; k < 3; k++) {
+      lo[k] = o.a[k] - r;
+      hi[k] = o.a[k] + r;
+    }
+    it.box.grow(lo);
+    it.box.grow(hi);
+    if (o.moving) {
+      for (int k = 0; k < 3; k++) {
+        lo[k] = o.b[k] - r;
+        hi[k] = o.b[k] + r;
+      }
+      it.box.grow(lo);
+      it.box.grow(hi);
+    }
+  } else {  // triangle.h:19-25
+    Tri<double> t{};
+    for (int k = 0; k < 3; k++) t.p0[k] = o.a[k];
+    v_sub(o.b, o.a, t.e1);
+    v_sub(o.c, o.a, t.e2);
+    double n[3];
+    v_cross(t.e1, t.e2, n);
+    v_unit(n, t.n);
+    t.mat = o.material;
+    tris_.push_back(t);
+    it.entry = mk(E_TRI, (uint32_t)tris_.size() - 1);
+    it.box.grow(o.a);
+    it.box.grow(o.b);
+    it.box.grow(o.c);
+  }
+  return it;
+}
+
+int Compiler::make_instance(const std::vector<Op>& chain, uint32_t blas) {
+  if ((int)chain.size() > kMaxChain) {
+    fail("more than " + std::to_string(kMaxChain) + " nested translate/rotate wrappers");
+    return -1;
+  }
+  Instance<double> in{};
+  in.nops = (int)chain.size();
+  for (size_t k = 0; k < chain.size(); k++) in.op[k] = {chain[k].x, chain[k].y, chain[k].z, chain[k].kind};
+  in.blas = blas;
+  insts_.push_back(in);
+  return (int)insts_.size() - 1;
+}
+
+Item Compiler::list_of(const std::vector<Item>& items) {
+  Item it{};
+  it.entry = mk(E_LIST, (uint32_t)refs_.size());
+  it.need = 0;
+  it.depth = 0;
+  it.volume = false;
+  for (const Item& m : items) {
+    refs_.push_back(m.entry);
+    it.box.grow(m.box);
+    uint32_t t = etype(m.entry);
+    if (t == E_INSTANCE || t == E_NODE || t == E_LIST) it.need = std::max(it.need, std::max(2, 1 + m.need));
+    it.depth = std::max(it.depth, m.depth);
+    it.volume = it.volume || m.volume;
+  }
+  refs_.push_back(kEnd);
+  return it;
+}
+
+Item Compiler::bvh(std::vector<Item>& items, size_t b, size_t e, int depth) {
+  size_t n = e - b;
+  if (n == 1) return items[b];
+  Box bounds, cb;
+  for (size_t i = b; i < e; i++) {
+    bounds.grow(items[i].box);
+    double c[3] = {items[i].box.center(0), items[i].box.center(1), items[i].box.center(2)};
+    cb.grow(c);
+  }
+  if (n <= (size_t)kLeafMax && depth > 0) {
+    std::vector<Item> leaf(items.begin() + (long)b, items.begin() + (long)e);
+    return list_of(leaf);
+  }
+  // binned SAH over the largest centroid axis
+  int axis = 0;
+  for (int k = 1; k < 3; k++)
+    if (cb.hi[k] - cb.lo[k] > cb.hi[axis] - cb.lo[axis]) axis = k;
+  size_t mid = b + n / 2;
+  double extent = cb.hi[axis] - cb.lo[axis];
+  bool split_found = false;
+  if (extent > 0 && depth < kMaxBvhDepth - 4) {
+    constexpr int kBins = 16;
+    Box bin_box[kBins];
+    size_t bin_cnt[kBins] = {};
+    auto bin_of = [&](const Item& it) {
+      int k = (int)((it.box.center(axis) - cb.lo[axis]) / extent * kBins);
+      return std::min(kBins - 1, std::max(0, k));
+    };
+    for (size_t i = b; i < e; i++) {
+      int k = bin_of(items[i]);
+      bin_cnt[k]++;
+      bin_box[k].grow(items[i].box);
+    }
+    double best = kInf;
+    int best_k = -1;
+    for (int s = 1; s < kBins; s++) {
+      Box lb, rb;
+      size_t lc = 0, rc = 0;
+      for (int k = 0; k < s; k++) {
+        lb.grow(bin_box[k]);
+        lc += bin_cnt[k];
+      }
+      for (int k = s; k < kBins; k++) {
+        rb.grow(bin_box[k]);
+        rc += bin_cnt[k];
+      }
+      if (!lc || !rc) continue;
+      double cost = lb.area() * (double)lc + rb.area() * (double)rc;
+      if (cost < best) {
+        best = cost;
+        best_k = s;
+      }
+    }
+    if (best_k > 0) {
+      double leaf_cost = bounds.area() * (double)n;
+      if (n <= (size_t)kLeafMax && best >= leaf_cost) {
+        std::vector<Item> leaf(items.begin() + (long)b, items.begin() + (long)e);
+        return list_of(leaf);
+      }
+      auto it = std::partition(items.begin() + (long)b, items.begin() + (long)e,
+                               [&](const Item& x) { return bin_of(x) < best_k; });
+      mid = (size_t)(it - items.begin());
+      split_found = mid > b && mid < e;
+    }
+  }
+  if (!split_found) {
+    mid = b + n / 2;
+    std::nth_element(items.begin() + (long)b, items.begin() + (long)mid, items.begin() + (long)e,
+                     [&](const Item& x, const Item& y) { return x.box.center(axis) < y.box.center(axis); });
+  }
+  size_t node_idx = nodes_.size();
+  nodes_.emplace_back();
+  Item l = bvh(items, b, mid, depth + 1);
+  Item r = bvh(items, mid, e, depth + 1);
+  Node<double>& nd = nodes_[node_idx];
+  for (int k = 0; k < 3; k++) {
+    nd.lo[0][k] = l.box.lo[k];
+    nd.hi[0][k] = l.box.hi[k];
+    nd.lo[1][k] = r.box.lo[k];
+    nd.hi[1][k] = r.box.hi[k];
+  }
+  nd.child[0] = l.entry;
+  nd.child[1] = r.entry;
+  Item it{};
+  it.entry = mk(E_NODE, (uint32_t)node_idx);
+  it.box = bounds;
+  it.need = std::max(2, 1 + std::max(l.need, r.need));
+  it.depth = 1 + std::max(l.depth, r.depth);
+  it.volume = l.volume || r.volume;
+  return it;
+}
+
+Item Compiler::container(std::vector<Item>& items, bool ordered) {
+  if (items.size() == 1) return items[0];
+  bool has_volume = false;
+  for (auto& i : items) has_volume = has_volume || i.volume;
+  if (ordered || has_volume || items.size() <= (size_t)kSmallList) return list_of(items);
+  return bvh(items, 0, items.size(), 0);
+}
+
+void Compiler::gather(int idx, const std::vector<Op>& chain, std::vector<Item>& out, bool ordered_ctx) {
+  if (!ok_) return;
+  if (++depth_guard_ > 4096) {
+    fail("object graph nesting too deep (cycle?)");
+    return;
+  }
+  const rt_object* o = obj(idx);
+  if (!o) return;
+  switch (o->kind) {
+    case RT_OBJ_QUAD:
+    case RT_OBJ_SPHERE:
+    case RT_OBJ_TRIANGLE:
+      out.push_back(prim_item(*o));
+      break;
+    case RT_OBJ_LIST:  // spliced in order: closest-hit over nested lists is the same scan
+      if (o->first_child < 0 || o->child_count < 0 || o->first_child + o->child_count > d_->num_children) {
+        fail("list child range out of bounds");
+        break;
+      }
+      for (int k = 0; k < o->child_count; k++) gather(d_->children[o->first_child + k], chain, out, ordered_ctx);
+      break;
+    case RT_OBJ_BVH: {
+      if (o->first_child < 0 || o->child_count < 0 || o->first_child + o->child_count > d_->num_children) {
+        fail("bvh child range out of bounds");
+        break;
+      }
+      std::vector<Item> sub;
+      for (int k = 0; k < o->child_count; k++) gather(d_->children[o->first_child + k], chain, sub, false);
+      if (!ok_) break;
+      if (!ordered_ctx) {
+        out.insert(out.end(), sub.begin(), sub.end());
+      } else if (!sub.empty()) {
+        out.push_back(sub.size() <= (size_t)kSmallList ? list_of(sub) : bvh(sub, 0, sub.size(), 0));
+      }
+      break;
+    }
+    case RT_OBJ_TRANSLATE:
+    case RT_OBJ_ROTATE_X:
+    case RT_OBJ_ROTATE_Y:
+    case RT_OBJ_ROTATE_Z: {
+      std::vector<Op> ops;
+      const rt_object* w = o;
+      while (w && is_wrapper(w->kind)) {
+        ops.push_back(op_of(*w));
+        w = obj(w->child);
+      }
+      if (!w) break;
+      std::vector<Op> chain2 = chain;
+      chain2.insert(chain2.end(), ops.begin(), ops.end());
+      std::vector<Item> sub;
+      gather((int)(w - d_->objects), chain2, sub, false);
+      if (!ok_) break;
+      Item blas = sub.empty() ? list_of(sub) : container(sub, false);
+      int ii = make_instance(chain2, blas.entry);
+      if (ii < 0) break;
+      Item it{};
+      it.entry = mk(E_INSTANCE, (uint32_t)ii);
+      it.box = box_to_parent(blas.box, ops);
+      it.need = std::max(2, 1 + blas.need);
+      it.depth = blas.depth;
+      it.volume = blas.volume;
+      out.push_back(it);
+      break;
+    }
+    case RT_OBJ_VOLUME: {
+      if (o->material < 0 || o->material >= d_->num_materials) {
+        fail("volume without a phase material");
+        break;
+      }
+      std::vector<Op> ops;
+      const rt_object* w = obj(o->child);
+      while (w && is_wrapper(w->kind)) {
+        ops.push_back(op_of(*w));
+        w = obj(w->child);
+      }
+      if (!w) break;
+      std::vector<Op> chain2 = chain;
+      chain2.insert(chain2.end(), ops.begin(), ops.end());
+      std::vector<Item> prims;
+      gather((int)(w - d_->objects), chain2, prims, true);
+      if (!ok_) break;
+      for (auto& p : prims) {
+        uint32_t t = etype(p.entry);
+        if (t != E_QUAD && t != E_SPHERE && t != E_TRI) {
+          fail("volume boundary must be primitives under one translate/rotate chain");
+          return;
+        }
+      }
+      Item bl = list_of(prims);
+      Volume<double> v{};
+      v.neg_inv_density = -1.0 / o->s0;
+      v.inst = chain2.empty() ? -1 : make_instance(chain2, bl.entry);
+      v.boundary = bl.entry;
+      v.phase_mat = o->material;
+      vols_.push_back(v);
+      Item it{};
+      it.entry = mk(E_VOLUME, (uint32_t)vols_.size() - 1);
+      it.box = box_to_parent(bl.box, ops);
+      it.need = 0;
+      it.depth = 0;
+      it.volume = true;
+      out.push_back(it);
+      break;
+    }
+    default:
+      fail("unsupported hittable kind " + std::to_string(o->kind));
+  }
+  --depth_guard_;
+}
+
+void Compiler::light_from(int idx) {
+  std::memset(&light_, 0, sizeof light_);
+  if (idx < 0) {
+    light_.kind = L_NONE;
+    return;
+  }
+  const rt_object* o = obj(idx);
+  if (!o) return;
+  if (o->kind == RT_OBJ_QUAD) {  // quad::pdf_value / random (quad.h:66-78)
+    size_t before = quads_.size();
+    Item it = prim_item(*o);
+    (void)it;
+    if (!ok_) return;
+    light_.kind = L_QUAD;
+    light_.quad = quads_.back();
+    quads_.resize(before);
+    for (int k = 0; k < 3; k++) {
+      light_.u[k] = o->b[k];
+      light_.v[k] = o->c[k];
+    }
+  } else if (o->kind == RT_OBJ_SPHERE) {  // sphere::pdf_value / random (sphere.h:76-81)
+    light_.kind = L_SPHERE;
+    for (int k = 0; k < 3; k++) light_.center[k] = o->moving ? 0.0 : o->a[k];
+    light_.radius = std::fmax(0, o->s0);
+  } else {
+    light_.kind = L_BASE;  // hittable base class: pdf_value 0, random (1,0,0) (hittable.h:39-41)
+  }
+}
+
+template <class T>
+size_t append(std::vector<unsigned char>& blob, const std::vector<T>& v) {
+  size_t off = (blob.size() + 255) & ~size_t(255);
+  blob.resize(off + v.size() * sizeof(T));
+  if (!v.empty()) std::memcpy(blob.data() + off, v.data(), v.size() * sizeof(T));
+  return off;
+}
+
+inline float down(double x) {
+  float f = (float)x;
+  if ((double)f > x) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
+  return std::nextafter(f, -std::numeric_limits<float>::infinity());
+}
+inline float up(double x) {
+  float f = (float)x;
+  if ((double)f < x) f = std::nextafter(f, std::numeric_limits<float>::infinity());
+  return std::nextafter(f, std::numeric_limits<float>::infinity());
+}
+
+template <class D, class S>
+void cvt3(D* d, const S* s) {
+  for (int k = 0; k < 3; k++) d[k] = (D)s[k];
+}
+
+Quad<float> to32(const Quad<double>& q) {
+  Quad<float> r{};
+  cvt3(r.n, q.n);
+  r.D = (float)q.D;
+  cvt3(r.q, q.q);
+  r.mat = q.mat;
+  cvt3(r.a, q.a);
+  r.area = (float)q.area;
+  cvt3(r.b, q.b);
+  return r;
+}
+Sphere<float> to32(const Sphere<double>& s) {
+  Sphere<float> r{};
+  cvt3(r.c1, s.c1);
+  r.r = (float)s.r;
+  cvt3(r.dc, s.dc);
+  r.mat = s.mat;
+  cvt3(r.cn, s.cn);
+  r.moving = s.moving;
+  return r;
+}
+Tri<float> to32(const Tri<double>& t) {
+  Tri<float> r{};
+  cvt3(r.p0, t.p0);
+  r.mat = t.mat;
+  cvt3(r.e1, t.e1);
+  cvt3(r.e2, t.e2);
+  cvt3(r.n, t.n);
+  return r;
+}
+Instance<float> to32(const Instance<double>& in) {
+  Instance<float> r{};
+  for (int k = 0; k < kMaxChain; k++) r.op[k] = {(float)in.op[k].x, (float)in.op[k].y, (float)in.op[k].z, in.op[k].kind};
+  r.nops = in.nops;
+  r.blas = in.blas;
+  return r;
+}
+Volume<float> to32(const Volume<double>& v) {
+  return {(float)v.neg_inv_density, v.inst, v.boundary, v.phase_mat};
+}
+Node<float> to32(const Node<double>& n) {
+  Node<float> r{};
+  for (int c = 0; c < 2; c++)
+    for (int k = 0; k < 3; k++) {
+      r.lo[c][k] = down(n.lo[c][k]);
+      r.hi[c][k] = up(n.hi[c][k]);
+    }
+  r.child[0] = n.child[0];
+  r.child[1] = n.child[1];
+  return r;
+}
+Material<float> to32(const Material<double>& m) { return {m.kind, m.tex, (float)m.fuzz, (float)m.refr}; }
+Texture<float> to32(const Texture<double>& t) {
+  Texture<float> r{};
+  cvt3(r.c0, t.c0);
+  r.kind = t.kind;
+  cvt3(r.c1, t.c1);
+  r.scale = (float)t.scale;
+  return r;
+}
+Light<float> to32(const Light<double>& l) {
+  Light<float> r{};
+  r.kind = l.kind;
+  r.quad = to32(l.quad);
+  cvt3(r.u, l.u);
+  cvt3(r.v, l.v);
+  cvt3(r.center, l.center);
+  r.radius = (float)l.radius;
+  return r;
+}
+template <class T>
+auto map32(const std::vector<T>& v) {
+  std::vector<decltype(to32(v[0]))> r;
+  r.reserve(v.size());
+  for (auto& x : v) r.push_back(to32(x));
+  return r;
+}
+
+template <class Q, class S, class T, class I, class V, class N, class M, class X, class L>
+SceneHeader pack(std::vector<unsigned char>& blob, const std::vector<Q>& q, const std::vector<S>& s,
+                 const std::vector<T>& t, const std::vector<I>& in, const std::vector<V>& vo, const std::vector<N>& nd,
+                 const std::vector<uint32_t>& refs, const std::vector<M>& m, const std::vector<X>& x, const L& light) {
+  SceneHeader h{};
+  blob.clear();
+  h.off_quads = append(blob, q);
+  h.off_spheres = append(blob, s);
+  h.off_tris = append(blob, t);
+  h.off_instances = append(blob, in);
+  h.off_volumes = append(blob, vo);
+  h.off_nodes = append(blob, nd);
+  h.off_refs = append(blob, refs);
+  h.off_mats = append(blob, m);
+  h.off_texs = append(blob, x);
+  h.off_light = append(blob, std::vector<L>{light});
+  blob.resize((blob.size() + 255) & ~size_t(255));
+  h.bytes = blob.size();
+  h.n_quads = (uint32_t)q.size();
+  h.n_spheres = (uint32_t)s.size();
+  h.n_tris = (uint32_t)t.size();
+  h.n_volumes = (uint32_t)vo.size();
+  h.n_nodes = (uint32_t)nd.size();
+  h.n_refs = (uint32_t)refs.size();
+  h.n_mats = (uint32_t)m.size();
+  h.n_texs = (uint32_t)x.size();
+  h.num_instances = (int32_t)in.size();
+  return h;
+}
+
+bool Compiler::run(CompiledScene* out, std::string* err) {
+  if (!d_) {
+    *err = "null scene descriptor";
+    return false;
+  }
+  // textures (texture.h:12-63) and materials (material.h:57-219)
+  for (int i = 0; i < d_->num_textures; i++) {
+    const rt_texture& t = d_->textures[i];
+    Texture<double> r{};
+    if (t.kind == RT_TEX_SOLID) {
+      r.kind = T_SOLID;
+      for (int k = 0; k < 3; k++) r.c0[k] = t.color[k];
+    } else if (t.kind == RT_TEX_CHECKER) {
+      r.kind = T_CHECKER;
+      for (int k = 0; k < 3; k++) {
+        r.c0[k] = t.odd[k];
+        r.c1[k] = t.even[k];
+      }
+      r.scale = t.scale;
+    } else {
+      *err = "texture kind " + std::to_string(t.kind) + " is not implemented on the device";
+      return false;
+    }
+    texs_.push_back(r);
+  }
+  for (int i = 0; i < d_->num_materials; i++) {
+    const rt_material& m = d_->materials[i];
+    if (m.texture < 0 || m.texture >= d_->num_textures) {
+      *err = "material " + std::to_string(i) + " has no valid texture";
+      return false;
+    }
+    if (m.kind < RT_MAT_LAMBERTIAN || m.kind > RT_MAT_DIFFUSE_LIGHT) {
+      *err = "material kind " + std::to_string(m.kind) + " is not implemented on the device";
+      return false;
+    }
+    mats_.push_back({m.kind, m.texture, (double)m.fuzz, (double)m.refraction});
+  }
+  if (d_->background >= d_->num_textures) {
+    *err = "background texture out of range";
+    return false;
+  }
+  std::vector<Item> top;
+  gather(d_->world, {}, top, false);
+  if (ok_) light_from(d_->light);
+  if (!ok_) {
+    *err = err_;
+    return false;
+  }
+  // the world object itself decides ordering: a list stays a list when it holds a volume or is small
+  const rt_object* w = &d_->objects[d_->world];
+  bool ordered = (w->kind == RT_OBJ_LIST);
+  Item root;
+  if (top.empty()) {
+    root = list_of(top);
+  } else if (ordered) {
+    root = container(top, false);
+  } else {
+    root = top.size() == 1 ? top[0] : bvh(top, 0, top.size(), 0);
+  }
+  if (root.need + 1 > kStackDepth) {
+    *err = "scene needs a deeper traversal stack than the device provides";
+    return false;
+  }
+  out->stack_need = std::max(1, root.need);
+  out->bvh_depth = root.depth;
+  out->num_items = (int)top.size();
+  out->hdr64 = pack(out->blob64, quads_, spheres_, tris_, insts_, vols_, nodes_, refs_, mats_, texs_, light_);
+  out->hdr = pack(out->blob32, map32(quads_), map32(spheres_), map32(tris_), map32(insts_), map32(vols_),
+                  map32(nodes_), refs_, map32(mats_), map32(texs_), to32(light_));
+  for (SceneHeader* h : {&out->hdr, &out->hdr64}) {
+    h->root = root.entry;
+    h->background = d_->background;
+    h->has_volumes = vols_.empty() ? 0 : 1;
+  }
+  return true;
+}
+
+}  // namespace
+
+rt_status compile_scene(const rt_scene_desc* desc, CompiledScene* out, std::string* err) {
+  if (!desc || !out || !err) return RT_ERR_INVALID_ARGUMENT;
+  if (desc->world < 0 || desc->world >= desc->num_objects) {
+    *err = "world object index out of range";
+    return RT_ERR_INVALID_ARGUMENT;
+  }
+  Compiler c(desc);
+  if (!c.run(out, err)) return RT_ERR_UNSUPPORTED;
+  return RT_OK;
+}
+
+}  // namespace rtd

@@ -1,0 +1,143 @@
+"""Python-side scene assembly onto the C ABI's rt_scene_desc.
+
+Mirrors the constructors of the reference's hittables/materials/textures
+(sphere.h, quad.h, triangle.h, hittable.h, hittable_list.h, bvh_node.h,
+volumne.h, material.h, texture.h) so tests can build arbitrary scenes. The
+production caller is the C++ plugin surface in ../../rt/ (camera::render).
+"""
+import math
+
+import numpy as np
+
+from . import abi
+
+
+class SceneBuilder:
+    def __init__(self):
+        self.objects, self.children, self.materials, self.textures = [], [], [], []
+
+    # textures (texture.h:12-63)
+    def solid(self, color):
+        t = abi.rt_texture(kind=abi.RT_TEX_SOLID)
+        t.color[:] = [float(c) for c in color]
+        self.textures.append(t)
+        return len(self.textures) - 1
+
+    def checker(self, odd, even, scale):
+        t = abi.rt_texture(kind=abi.RT_TEX_CHECKER, scale=float(scale))
+        t.odd[:] = [float(c) for c in odd]
+        t.even[:] = [float(c) for c in even]
+        self.textures.append(t)
+        return len(self.textures) - 1
+
+    # materials (material.h)
+    def _mat(self, kind, tex, fuzz=0.0, refraction=1.0):
+        self.materials.append(abi.rt_material(kind=kind, texture=tex, fuzz=fuzz, refraction=refraction))
+        return len(self.materials) - 1
+
+    def lambertian(self, tex):
+        return self._mat(abi.RT_MAT_LAMBERTIAN, tex)
+
+    def metal(self, tex, fuzz=0.0):  # fuzz clamped to [0,1] (material.h:80-82)
+        return self._mat(abi.RT_MAT_METAL, tex, fuzz=min(1.0, max(0.0, fuzz)))
+
+    def dielectric(self, tex, refraction):
+        return self._mat(abi.RT_MAT_DIELECTRIC, tex, refraction=refraction)
+
+    def isotropic(self, tex):
+        return self._mat(abi.RT_MAT_ISOTROPIC, tex)
+
+    def diffuse_light(self, tex):
+        return self._mat(abi.RT_MAT_DIFFUSE_LIGHT, tex)
+
+    # hittables
+    def _obj(self, **kw):
+        o = abi.rt_object(material=-1, child=-1, first_child=0, child_count=0)
+        for k, v in kw.items():
+            if k in ("a", "b", "c"):
+                getattr(o, k)[:] = [float(x) for x in v]
+            else:
+                setattr(o, k, v)
+        self.objects.append(o)
+        return len(self.objects) - 1
+
+    def sphere(self, center, radius, mat):
+        return self._obj(kind=abi.RT_OBJ_SPHERE, a=center, s0=float(radius), material=mat)
+
+    def moving_sphere(self, c1, c2, radius, mat):
+        return self._obj(kind=abi.RT_OBJ_SPHERE, a=c1, b=c2, s0=float(radius), material=mat, moving=1)
+
+    def quad(self, q, u, v, mat):
+        return self._obj(kind=abi.RT_OBJ_QUAD, a=q, b=u, c=v, material=mat)
+
+    def triangle(self, p0, p1, p2, mat):
+        return self._obj(kind=abi.RT_OBJ_TRIANGLE, a=p0, b=p1, c=p2, material=mat)
+
+    def _group(self, kind, members):
+        first = len(self.children)
+        self.children.extend(members)
+        return self._obj(kind=kind, first_child=first, child_count=len(members))
+
+    def hlist(self, members):
+        return self._group(abi.RT_OBJ_LIST, list(members))
+
+    def bvh(self, members):
+        return self._group(abi.RT_OBJ_BVH, list(members))
+
+    def translate(self, obj, offset):
+        return self._obj(kind=abi.RT_OBJ_TRANSLATE, child=obj, a=offset)
+
+    def rotate(self, axis, obj, degrees):  # hittable.h:95-98 sin/cos of degrees_to_radians
+        rad = degrees * math.pi / 180.0
+        kind = {0: abi.RT_OBJ_ROTATE_X, 1: abi.RT_OBJ_ROTATE_Y, 2: abi.RT_OBJ_ROTATE_Z}[axis]
+        return self._obj(kind=kind, child=obj, s0=math.sin(rad), s1=math.cos(rad))
+
+    def volume(self, boundary, density, tex):  # volumne.h:11-15 makes an isotropic phase function
+        return self._obj(kind=abi.RT_OBJ_VOLUME, child=boundary, s0=float(density), material=self.isotropic(tex))
+
+    def box_members(self, a, b, mat):  # quad.h:91-112
+        mn = [min(a[i], b[i]) for i in range(3)]
+        mx = [max(a[i], b[i]) for i in range(3)]
+        dx, dy, dz = (mx[0] - mn[0], 0, 0), (0, mx[1] - mn[1], 0), (0, 0, mx[2] - mn[2])
+        neg = lambda v: tuple(-x for x in v)
+        return [self.quad((mn[0], mn[1], mx[2]), dy, dx, mat), self.quad((mx[0], mn[1], mx[2]), dy, neg(dz), mat),
+                self.quad((mx[0], mn[1], mn[2]), dy, neg(dx), mat), self.quad((mn[0], mn[1], mn[2]), dy, dz, mat),
+                self.quad((mn[0], mx[1], mx[2]), neg(dz), dx, mat), self.quad((mn[0], mn[1], mn[2]), dz, dx, mat)]
+
+    def box(self, a, b, mat):
+        return self.hlist(self.box_members(a, b, mat))
+
+    def desc(self, world, light=-1, background=-1):
+        """The rt_scene_desc; the returned object keeps the arrays alive."""
+        d = abi.rt_scene_desc()
+        self._keep = (
+            (abi.rt_object * max(1, len(self.objects)))(*self.objects),
+            (abi.c_int32 * max(1, len(self.children)))(*self.children),
+            (abi.rt_material * max(1, len(self.materials)))(*self.materials),
+            (abi.rt_texture * max(1, len(self.textures)))(*self.textures),
+        )
+        d.objects, d.children, d.materials, d.textures = self._keep
+        d.num_objects, d.num_children = len(self.objects), len(self.children)
+        d.num_materials, d.num_textures = len(self.materials), len(self.textures)
+        d.world, d.light, d.background = world, light, background
+        d._owner = self
+        return d
+
+
+def perspective(image_width, aspect, pos, lookat, focal_length=1.0, fovy_degree=90.0):
+    """camera::initialize_perspective (camera.h:21-50), including its float-typed fovy/theta/focal."""
+    pos, lookat = np.asarray(pos, float), np.asarray(lookat, float)
+    unit = lambda v: v / math.sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2])
+    cross = lambda a, b: np.array([a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]])
+    d = unit(lookat - pos)
+    right = unit(cross(d, np.array([0.0, 1.0, 0.0])))
+    up = cross(right, d)
+    focal = float(np.float32(focal_length))
+    h = max(1, int(image_width / aspect))
+    theta = float(np.float32(float(np.float32(fovy_degree)) * math.pi / 180.0))
+    vh = 2.0 * math.tan(theta / 2.0) * focal
+    vw = vh * (float(image_width) / h)
+    c = abi.rt_camera_desc(mode=abi.RT_CAM_PERSPECTIVE, image_width=image_width, image_height=h,
+                           viewport_width=vw, viewport_height=vh, focal_length=focal, focus_dist=3.4)
+    c.pos[:], c.dir[:], c.right[:], c.up[:] = list(pos), list(d), list(right), list(up)
+    return c
