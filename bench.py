@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""Msamples/s of the MI355X wavefront path tracer on BASELINE.json's headline config.
+
+Workload (BASELINE.json configs[1]): the reference's Cornell Box
+(main.cc:198-225) at 800x800, 1024 spp, max depth 50, light importance sampling on.
+One step = one full frame. The framebuffer is cut into 64x64 tiles dealt
+round-robin to the ranks; each rank renders its tiles on its GPU and rank 0
+gathers them (RCCL, torch.distributed "nccl") into the full linear framebuffer.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "cpu-ray-tracing-implementation_amd", "python"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import rt_amd  # noqa: E402
+from rt_amd import abi, scenes  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+# SURVEY.md §8(d) algorithmic bytes: per sample (generate + finalise) and per segment
+B_GEN, B_ACC, B_EXT, B_SHADE = 64, 36, 44, 152
+
+CONFIGS = {
+    # name: (scene, width, aspect, spp, depth)
+    "c1": ("cornell_box", 400, 1.0, 64, 8),
+    "c2": ("cornell_box", 800, 1.0, 1024, 50),
+    "c3": ("rtow", 1200, 1.5, 512, 50),
+    "c5": ("cornell_box_with_volume", 3840, 16.0 / 9.0, 4096, 5),
+}
+
+
+def tiles_of(w, h, rank, world, ts=64):
+    all_tiles = [(x, y, min(ts, w - x), min(ts, h - y)) for y in range(0, h, ts) for x in range(0, w, ts)]
+    return all_tiles[rank::world]
+
+
+def pixel_index(tiles, w):
+    idx = []
+    for (x0, y0, tw, th) in tiles:
+        ys, xs = np.mgrid[y0:y0 + th, x0:x0 + tw]
+        idx.append((ys * w + xs).reshape(-1))
+    return np.concatenate(idx) if idx else np.zeros(0, dtype=np.int64)
+
+
+def cpu_baseline(scene_name, width, aspect, spp, depth, seed, threads):
+    """The oracle (fp64 restatement of the reference loop) on host cores, over a row sample."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    desc, cam, _, _ = scenes.SCENES[scene_name](width=width, aspect=aspect)
+    osc = oracle.from_desc(desc)
+    # about 80 Msamples (a few seconds on 16 cores): evenly spaced full rows at the full spp and depth
+    nrows = max(1, min(cam.image_height, int(80e6 // (cam.image_width * spp))))
+    step = cam.image_height // nrows
+    rows = list(range(0, cam.image_height, step))[:nrows]
+    tiles = [(0, y, cam.image_width, 1) for y in rows]
+    t0 = time.perf_counter()
+    oracle.render(osc, cam, spp, depth, seed=seed, threads=threads, tiles=tiles)
+    dt = time.perf_counter() - t0
+    n = len(rows) * cam.image_width * spp
+    return {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"oracle (fp64 C++ restatement, counter RNG) on {len(rows)} rows (every {step}th) x "
+                      f"{cam.image_width} px x {spp} spp, depth {depth}: {n / 1e6:.1f} Msamples in {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
+    ap.add_argument("--pool", type=int, default=0, help="wavefront slots (0 = library default)")
+    ap.add_argument("--chunk", type=int, default=0, help="samples per work item (0 = library default)")
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--kernel-timing", default="on", choices=["on", "off"],
+                    help="HIP events around every extend/shade launch of the timed steps (roofline)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    scene_name, width, aspect, spp, depth = CONFIGS[args.config]
+    desc, cam, _, _ = scenes.SCENES[scene_name](width=width, aspect=aspect)
+    W, H = cam.image_width, cam.image_height
+    prec = abi.RT_PREC_F64 if args.precision == "f64" else abi.RT_PREC_F32
+    tdtype = torch.float64 if prec == abi.RT_PREC_F64 else torch.float32
+
+    ctx = rt_amd.Context(local)
+    ctx.upload(desc)
+    my_tiles = tiles_of(W, H, rank, world)
+    all_tiles = [tiles_of(W, H, r, world) for r in range(world)]
+    counts = [sum(t[2] * t[3] for t in ts) for ts in all_tiles]
+    maxpix = max(counts)
+    out = torch.zeros((maxpix, 3), dtype=tdtype, device=dev)
+    params = ctx.params(spp, depth, args.seed, prec, samples_per_item=args.chunk, pool_slots=args.pool)
+    fb = gathered = scatter_idx = None
+    if rank == 0:
+        fb = torch.zeros((H * W, 3), dtype=tdtype, device=dev)
+        gathered = [torch.zeros_like(out) for _ in range(world)]
+        scatter_idx = [torch.from_numpy(pixel_index(all_tiles[r], W)).to(dev) for r in range(world)]
+
+    def step():
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        ctx.render_tiles(cam, params, my_tiles, out.data_ptr(), 1, stream)
+        if world > 1:
+            dist.gather(out, gathered if rank == 0 else None, dst=0)
+            parts = gathered
+        else:
+            parts = [out]
+        if rank == 0:
+            for r in range(world):
+                fb[scatter_idx[r]] = parts[r][: counts[r]]
+
+    for _ in range(args.warmup):
+        step()
+    ctx.set_timing(args.kernel_timing == "on")
+    ctx.reset_counters()
+    ext_ms = sh_ms = 0.0
+    iters = 0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        st = ctx.stats()
+        ext_ms += st.extend_ms
+        sh_ms += st.shade_ms
+        iters += st.iterations
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st = ctx.stats()
+    segs = st.segments
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        s = torch.tensor([segs], dtype=torch.float64, device=dev)
+        dist.all_reduce(s, op=dist.ReduceOp.SUM)
+        segs_total = float(s.item())
+    else:
+        segs_total = float(segs)
+
+    total_samples = W * H * spp * args.steps
+    value = total_samples / elapsed / 1e6
+    if rank == 0:
+        my_samples = counts[0] * spp * args.steps
+        seg_per_sample = segs / max(1, my_samples)
+        # dominant kernel of rank 0: per-launch algorithmic bytes / average launch duration (HIP events)
+        roof = None
+        if args.kernel_timing == "on" and iters > 0:
+            kern, ms, bpseg = ("shade", sh_ms, B_SHADE) if sh_ms >= ext_ms else ("extend", ext_ms, B_EXT)
+            avg_s = ms / 1e3 / iters
+            bytes_per_launch = bpseg * segs / iters
+            achieved = bytes_per_launch / avg_s / 1e9
+            roof = {"bound": "hbm", "kernel": f"k_{kern}", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "avg_launch_us": round(avg_s * 1e6, 2), "launches": iters,
+                    "alg_bytes_per_launch": int(bytes_per_launch),
+                    "whole_job_alg_GBs": round((B_GEN + B_ACC + (B_EXT + B_SHADE) * seg_per_sample) *
+                                               my_samples / elapsed / 1e9, 1)}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(scene_name, width, aspect, spp, depth, args.seed, args.cpu_threads)
+        line = {
+            "metric": "Msamples/sec (pixels*spp) Cornell Box 800x800@1024spp; 1/2/4/8-GPU scaling"
+            if args.config == "c2" else f"Msamples/sec (pixels*spp) {scene_name} {W}x{H}@{spp}spp",
+            "value": round(value, 2), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "fp32" if prec == abi.RT_PREC_F32 else "fp64",
+            "data": "synthetic (the reference's Cornell Box scene, procedurally built; no assets)",
+            "config": {"workload": f"{scene_name} {W}x{H} {spp}spp depth {depth}, light sampling on",
+                       "image": [W, H], "spp": spp, "max_depth": depth, "tiles": "64x64 round-robin over ranks",
+                       "parallelism": f"tiles{world}", "segments_per_sample": round(seg_per_sample, 4),
+                       "segments_total": segs_total / args.steps, "kernel_timing": args.kernel_timing,
+                       "rounds_per_frame": iters // max(1, args.steps)},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        if cpu:
+            line["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

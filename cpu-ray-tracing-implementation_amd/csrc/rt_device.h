@@ -80,6 +80,10 @@ __device__ __forceinline__ V<R> refract(V<R> v, V<R> n, R eta) {  // utility.h:7
   return perp + par;
 }
 
+// a / b: exact IEEE division for the fp64 parity path, v_rcp_f32-based for the fp32 path
+__device__ __forceinline__ float fdiv(float a, float b) { return __fdividef(a, b); }
+__device__ __forceinline__ double fdiv(double a, double b) { return a / b; }
+
 template <class R>
 struct Num;
 template <>
@@ -146,6 +150,8 @@ struct DevScene {
   const Material<R>* mats;
   const Texture<R>* texs;
   const Light<R>* light;
+  const uint32_t* linear;
+  uint32_t n_linear;
   uint32_t root;
   int32_t background;
   int32_t has_volumes;
@@ -202,7 +208,7 @@ __device__ __forceinline__ bool box_hit(const R* lo, const R* hi, V<R> o, V<R> i
 template <class R>
 __device__ __forceinline__ bool quad_t(const Quad<R>& q, V<R> o, V<R> d, R tmin, R tmax, R& t) {
   V<R> n = ld3(q.n);
-  R th = (q.D - dot(n, o)) / dot(n, d);
+  R th = fdiv(q.D - dot(n, o), dot(n, d));
   if (!(tmin <= th && th <= tmax)) return false;  // interval::is_contains, NaN fails
   V<R> p = (o + th * d) - ld3(q.q);
   R a = dot(p, ld3(q.a)), b = dot(p, ld3(q.b));
@@ -217,8 +223,14 @@ __device__ __forceinline__ bool tri_t(const Tri<R>& tr, V<R> o, V<R> d, R tmin, 
   V<R> e1 = ld3(tr.e1), e2 = ld3(tr.e2);
   V<R> s = o - ld3(tr.p0);
   V<R> s1 = cross(d, e2), s2 = cross(s, e1);
-  R den = dot(s1, e1);
-  R th = dot(s2, e2) / den, b0 = dot(s1, s) / den, b1 = dot(s2, d) / den;
+  R inv = fdiv(R(1), dot(s1, e1));
+  R th = dot(s2, e2) * inv, b0 = dot(s1, s) * inv, b1 = dot(s2, d) * inv;
+  if (sizeof(R) == 8) {  // the parity path divides like triangle.h:14
+    R den = dot(s1, e1);
+    th = dot(s2, e2) / den;
+    b0 = dot(s1, s) / den;
+    b1 = dot(s2, d) / den;
+  }
   if (th < tmin || th > tmax) return false;
   if (b0 < R(0) || b1 < R(0) || b0 + b1 > R(1)) return false;
   if (th != th) return false;  // 0/0 determinant: the reference's comparisons reject NaN too
@@ -300,15 +312,13 @@ __device__ bool list_closest(const DevScene<R>& sc, uint32_t pos, V<R> o, V<R> d
 }
 
 // volumne::hit (volumne.h:18-46). o, d: the ray as the volume sees it.
+// wo, wd: the world ray (the boundary's wrapper chain is absolute, world -> boundary space);
+// d: the ray as the volume itself sees it (its length scales the free-flight distance).
 template <class R>
-__device__ bool volume_t(const DevScene<R>& sc, const Volume<R>& v, V<R> o, V<R> d, R time, R tmin, R tmax, Keys k,
-                         uint32_t bounce, uint32_t& jv, R& t) {
-  V<R> bo = o, bd = d;
-  if (v.inst >= 0) {
-    // the boundary chain is absolute (world -> boundary); volumes live at the level their chain starts
-    // from, which the compiler guarantees is the world for top-level volumes.
-    chain_in(sc.insts[v.inst], bo, bd);
-  }
+__device__ bool volume_t(const DevScene<R>& sc, const Volume<R>& v, V<R> wo, V<R> wd, V<R> d, R time, R tmin,
+                         R tmax, Keys k, uint32_t bounce, uint32_t& jv, R& t) {
+  V<R> bo = wo, bd = wd;
+  if (v.inst >= 0) chain_in(sc.insts[v.inst], bo, bd);
   R t1, t2;
   if (!list_closest(sc, epay(v.boundary), bo, bd, time, -Num<R>::inf(), Num<R>::inf(), t1)) return false;
   if (!list_closest(sc, epay(v.boundary), bo, bd, time, t1 + R(0.0001), Num<R>::inf(), t2)) return false;
@@ -366,7 +376,7 @@ __device__ void trace(const DevScene<R>& sc, V<R> wo, V<R> wd, R time, uint32_t 
   };
   auto test_volume = [&](uint32_t e) {
     R th;
-    if (volume_t(sc, sc.vols[epay(e)], o, d, time, tmin, tmax, keys, bounce, jv, th)) {
+    if (volume_t(sc, sc.vols[epay(e)], wo, wd, d, time, tmin, tmax, keys, bounce, jv, th)) {
       tmax = th;
       e_best = e;
       i_best = cur;
@@ -431,6 +441,52 @@ __device__ void trace(const DevScene<R>& sc, V<R> wo, V<R> wd, R time, uint32_t 
       d = wd;
       if (cur >= 0) chain_in(sc.insts[cur], o, d);
       inv = mkv(R(1) / d.x, R(1) / d.y, R(1) / d.z);
+    }
+  }
+  t_best = tmax;
+}
+
+// Linear program (small scenes, rt_scene.h): every lane walks the same ops, so
+// the loop, the op and the primitive records are wave-uniform (scalar loads).
+template <class R, bool SPH, bool TRI, bool VOL>
+__device__ __forceinline__ void trace_linear(const DevScene<R>& sc, V<R> wo, V<R> wd, R time, uint32_t excl_e,
+                                             int32_t excl_i, Keys keys, uint32_t bounce, R& t_best,
+                                             uint32_t& e_best, int32_t& i_best) {
+  const R tmin = R(0.001);
+  R tmax = Num<R>::inf();
+  V<R> o = wo, d = wd;
+  int32_t cur = -1;
+  uint32_t jv = 0;
+  e_best = kNoHit;
+  i_best = -1;
+  const uint32_t n = sc.n_linear;
+  for (uint32_t k = 0; k < n; k++) {
+    const uint32_t op = sc.linear[k];
+    const uint32_t ty = etype(op), idx = epay(op);
+    R th;
+    bool h = false;
+    if (ty == E_QUAD) {
+      if (!(op == excl_e && cur == excl_i)) h = quad_t(sc.quads[idx], o, d, tmin, tmax, th);
+    } else if (SPH && ty == E_SPHERE) {
+      h = sphere_t(sc.spheres[idx], o, d, time, tmin, tmax, op == excl_e && cur == excl_i, th);
+    } else if (TRI && ty == E_TRI) {
+      if (!(op == excl_e && cur == excl_i)) h = tri_t(sc.tris[idx], o, d, tmin, tmax, th);
+    } else if (ty == E_INSTANCE) {
+      cur = (int32_t)idx;
+      o = wo;
+      d = wd;
+      chain_in(sc.insts[idx], o, d);
+    } else if (VOL && ty == E_VOLUME) {
+      h = volume_t(sc, sc.vols[idx], wo, wd, d, time, tmin, tmax, keys, bounce, jv, th);
+    } else {  // kInstEnd
+      cur = -1;
+      o = wo;
+      d = wd;
+    }
+    if (h) {
+      tmax = th;
+      e_best = op;
+      i_best = cur;
     }
   }
   t_best = tmax;

@@ -74,6 +74,7 @@ struct Params {
   uint64_t seed;
   V<R> pos, du, dv, dir00;
   unsigned long long* seg_shards;
+  bool feat_sph, feat_tri;  // scene has spheres / triangles (selects the linear kernel variant)
 };
 
 // ------------------------------------------------------------------ camera ray (camera.h:244-251,293)
@@ -155,6 +156,42 @@ __global__ __launch_bounds__(kBlock) void k_extend(Params<R> p) {
     p.H[slot] = h;
   }
   // segments traced: one count per wave, one atomic per block
+  unsigned long long m = __ballot(active);
+  int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) wave_cnt[wave] = (uint32_t)__popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t c = 0;
+    for (int w = 0; w < kBlock / 64; w++) c += wave_cnt[w];
+    if (c) atomicAdd(&p.seg_shards[blockIdx.x % kSegShards], (unsigned long long)c);
+  }
+}
+
+template <class R, bool SPH, bool TRI, bool VOL>
+__global__ __launch_bounds__(kBlock) void k_extend_linear(Params<R> p) {
+  __shared__ uint32_t wave_cnt[kBlock / 64];
+  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  bool active = i < p.n;
+  uint32_t slot = 0;
+  R4<R> Dv{};
+  if (active) {
+    slot = p.queue ? p.queue[i] : i;
+    Dv = p.D[slot];
+    active = Dv.w >= R(0);
+  }
+  if (active) {
+    R4<R> Ov = p.O[slot];
+    HitRec<R> prev = p.H[slot];
+    Keys k{0, 0};
+    if (VOL) {
+      uint4 s = p.S[slot];
+      k = {s.x, s.y};
+    }
+    HitRec<R> h;
+    trace_linear<R, SPH, TRI, VOL>(p.sc, mkv(Ov.x, Ov.y, Ov.z), mkv(Dv.x, Dv.y, Dv.z), Ov.w, prev.e, prev.i, k,
+                                   (uint32_t)Dv.w, h.t, h.e, h.i);
+    p.H[slot] = h;
+  }
   unsigned long long m = __ballot(active);
   int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (lane == 0) wave_cnt[wave] = (uint32_t)__popcll(m);
@@ -550,6 +587,8 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
   s.mats = (const Material<R>*)at(h.off_mats);
   s.texs = (const Texture<R>*)at(h.off_texs);
   s.light = (const Light<R>*)at(h.off_light);
+  s.linear = (const uint32_t*)at(h.off_linear);
+  s.n_linear = h.n_linear;
   s.root = h.root;
   s.background = h.background;
   s.has_volumes = h.has_volumes;
@@ -558,6 +597,20 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
 
 template <class R>
 void launch_extend2(const Params<R>& p, int stack, uint32_t grid, hipStream_t st) {
+  if (p.sc.n_linear > 0) {
+    const bool sph = p.feat_sph, tri = p.feat_tri, vol = p.sc.has_volumes != 0;
+#define RT_LIN(S, T, V) hipLaunchKernelGGL((k_extend_linear<R, S, T, V>), dim3(grid), dim3(kBlock), 0, st, p)
+    if (!sph && !tri && !vol)
+      RT_LIN(false, false, false);
+    else if (!sph && !tri && vol)
+      RT_LIN(false, false, true);
+    else if (sph && !tri && !vol)
+      RT_LIN(true, false, false);
+    else
+      RT_LIN(true, true, true);
+#undef RT_LIN
+    return;
+  }
   if (stack <= 8)
     hipLaunchKernelGGL((k_extend<R, 8>), dim3(grid), dim3(kBlock), 0, st, p);
   else if (stack <= 16)
@@ -648,6 +701,8 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     p.dv = tov<R>(vw.dv);
     p.dir00 = tov<R>(vw.dir00);
     p.seg_shards = (unsigned long long*)c->counters.ptr;
+    p.feat_sph = hdr.n_spheres > 0;
+    p.feat_tri = hdr.n_tris > 0;
 
     hipLaunchKernelGGL(k_init<R>, dim3(nblk_max), dim3(kBlock), 0, st, p);
     uint64_t launches = 1, iters = 0;

@@ -44,6 +44,11 @@ __host__ __device__ inline uint32_t mk(uint32_t type, uint32_t payload) { return
 constexpr int kMaxChain = 4;    // translate/rotate wrappers per instance (composed, outermost first)
 constexpr int kStackDepth = 32;  // traversal stack entries per lane (LDS)
 constexpr int kMaxBvhDepth = 26; // the builder keeps every BVH within this depth
+// Small scenes also get a *linear program*: every top-level item in the reference's
+// list order -- primitive entries, INSTANCE(i) ... kInstEnd brackets, VOLUME(i) --
+// that all lanes of a wave walk in lock-step (wave-uniform, scalar-loaded records).
+constexpr int kLinearMax = 96;
+constexpr uint32_t kInstEnd = kRestoreBase;  // back to the world ray
 
 // quad.h:9-23 precomputed: n = unit(cross(u,v)), D = dot(n, corner),
 // a = cross(v, w), b = cross(w, u) with w = cross(u,v)/dot(cross(u,v),cross(u,v)),
@@ -160,8 +165,10 @@ struct SceneHeader {
   int32_t has_volumes;
   int32_t num_instances;
   uint64_t off_quads, off_spheres, off_tris, off_instances, off_volumes, off_nodes, off_refs, off_mats, off_texs,
-      off_light;
+      off_light, off_linear;
   uint64_t bytes;
+  uint32_t n_linear;  // 0: no linear program (use the BVH traversal)
+  uint32_t pad_;
   uint32_t n_quads, n_spheres, n_tris, n_volumes, n_nodes, n_refs, n_mats, n_texs;
 };
 

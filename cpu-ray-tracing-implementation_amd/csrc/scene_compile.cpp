@@ -109,7 +109,23 @@ struct Item {
   int need;   // traversal stack entries processing this entry can add
   int depth;  // BVH depth below this entry
   bool volume;
+  bool lin_ok = true;         // the item has a linear-program form (see rt_scene.h)
+  std::vector<uint32_t> lin;  // its ops in reference order
 };
+
+// concatenation of the items' linear programs, in order
+void join_lin(Item& dst, const std::vector<Item>& items) {
+  dst.lin.clear();
+  dst.lin_ok = true;
+  for (const Item& m : items) {
+    if (!m.lin_ok || dst.lin.size() + m.lin.size() > (size_t)kLinearMax) {
+      dst.lin_ok = false;
+      dst.lin.clear();
+      return;
+    }
+    dst.lin.insert(dst.lin.end(), m.lin.begin(), m.lin.end());
+  }
+}
 
 class Compiler {
  public:
@@ -239,6 +255,7 @@ Item Compiler::prim_item(const rt_object& o) {
     it.box.grow(o.b);
     it.box.grow(o.c);
   }
+  it.lin = {it.entry};
   return it;
 }
 
@@ -270,6 +287,7 @@ Item Compiler::list_of(const std::vector<Item>& items) {
     it.volume = it.volume || m.volume;
   }
   refs_.push_back(kEnd);
+  join_lin(it, items);
   return it;
 }
 
@@ -359,6 +377,7 @@ Item Compiler::bvh(std::vector<Item>& items, size_t b, size_t e, int depth) {
   Item it{};
   it.entry = mk(E_NODE, (uint32_t)node_idx);
   it.box = bounds;
+  it.lin_ok = false;  // a BVH's linear form comes from its items in reference order (container())
   it.need = std::max(2, 1 + std::max(l.need, r.need));
   it.depth = 1 + std::max(l.depth, r.depth);
   it.volume = l.volume || r.volume;
@@ -370,7 +389,12 @@ Item Compiler::container(std::vector<Item>& items, bool ordered) {
   bool has_volume = false;
   for (auto& i : items) has_volume = has_volume || i.volume;
   if (ordered || has_volume || items.size() <= (size_t)kSmallList) return list_of(items);
-  return bvh(items, 0, items.size(), 0);
+  Item lin_src;
+  join_lin(lin_src, items);  // reference (gather) order, before the BVH build reorders
+  Item it = bvh(items, 0, items.size(), 0);
+  it.lin = std::move(lin_src.lin);
+  it.lin_ok = lin_src.lin_ok;
+  return it;
 }
 
 void Compiler::gather(int idx, const std::vector<Op>& chain, std::vector<Item>& out, bool ordered_ctx) {
@@ -405,7 +429,7 @@ void Compiler::gather(int idx, const std::vector<Op>& chain, std::vector<Item>& 
       if (!ordered_ctx) {
         out.insert(out.end(), sub.begin(), sub.end());
       } else if (!sub.empty()) {
-        out.push_back(sub.size() <= (size_t)kSmallList ? list_of(sub) : bvh(sub, 0, sub.size(), 0));
+        out.push_back(container(sub, sub.size() <= (size_t)kSmallList));
       }
       break;
     }
@@ -434,6 +458,16 @@ void Compiler::gather(int idx, const std::vector<Op>& chain, std::vector<Item>& 
       it.need = std::max(2, 1 + blas.need);
       it.depth = blas.depth;
       it.volume = blas.volume;
+      it.lin_ok = blas.lin_ok;
+      for (uint32_t op : blas.lin)
+        if (etype(op) == E_INSTANCE) it.lin_ok = false;  // nested instances: BVH traversal only
+      if (it.lin_ok && blas.lin.size() + 2 <= (size_t)kLinearMax) {
+        it.lin.push_back(it.entry);
+        it.lin.insert(it.lin.end(), blas.lin.begin(), blas.lin.end());
+        it.lin.push_back(kInstEnd);
+      } else {
+        it.lin_ok = false;
+      }
       out.push_back(it);
       break;
     }
@@ -474,6 +508,7 @@ void Compiler::gather(int idx, const std::vector<Op>& chain, std::vector<Item>& 
       it.need = 0;
       it.depth = 0;
       it.volume = true;
+      it.lin = {it.entry};
       out.push_back(it);
       break;
     }
@@ -617,7 +652,8 @@ auto map32(const std::vector<T>& v) {
 template <class Q, class S, class T, class I, class V, class N, class M, class X, class L>
 SceneHeader pack(std::vector<unsigned char>& blob, const std::vector<Q>& q, const std::vector<S>& s,
                  const std::vector<T>& t, const std::vector<I>& in, const std::vector<V>& vo, const std::vector<N>& nd,
-                 const std::vector<uint32_t>& refs, const std::vector<M>& m, const std::vector<X>& x, const L& light) {
+                 const std::vector<uint32_t>& refs, const std::vector<M>& m, const std::vector<X>& x, const L& light,
+                 const std::vector<uint32_t>& linear) {
   SceneHeader h{};
   blob.clear();
   h.off_quads = append(blob, q);
@@ -630,6 +666,8 @@ SceneHeader pack(std::vector<unsigned char>& blob, const std::vector<Q>& q, cons
   h.off_mats = append(blob, m);
   h.off_texs = append(blob, x);
   h.off_light = append(blob, std::vector<L>{light});
+  h.off_linear = append(blob, linear);
+  h.n_linear = (uint32_t)linear.size();
   blob.resize((blob.size() + 255) & ~size_t(255));
   h.bytes = blob.size();
   h.n_quads = (uint32_t)q.size();
@@ -707,12 +745,16 @@ bool Compiler::run(CompiledScene* out, std::string* err) {
     *err = "scene needs a deeper traversal stack than the device provides";
     return false;
   }
+  Item lin_top;
+  join_lin(lin_top, top);
+  std::vector<uint32_t> linear;
+  if (lin_top.lin_ok) linear = lin_top.lin;
   out->stack_need = std::max(1, root.need);
   out->bvh_depth = root.depth;
   out->num_items = (int)top.size();
-  out->hdr64 = pack(out->blob64, quads_, spheres_, tris_, insts_, vols_, nodes_, refs_, mats_, texs_, light_);
+  out->hdr64 = pack(out->blob64, quads_, spheres_, tris_, insts_, vols_, nodes_, refs_, mats_, texs_, light_, linear);
   out->hdr = pack(out->blob32, map32(quads_), map32(spheres_), map32(tris_), map32(insts_), map32(vols_),
-                  map32(nodes_), refs_, map32(mats_), map32(texs_), to32(light_));
+                  map32(nodes_), refs_, map32(mats_), map32(texs_), to32(light_), linear);
   for (SceneHeader* h : {&out->hdr, &out->hdr64}) {
     h->root = root.entry;
     h->background = d_->background;
