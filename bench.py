@@ -82,6 +82,8 @@ def main():
     ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
     ap.add_argument("--pool", type=int, default=0, help="wavefront slots (0 = library default)")
     ap.add_argument("--chunk", type=int, default=0, help="samples per work item (0 = library default)")
+    ap.add_argument("--segments-per-launch", type=int, default=0,
+                    help="segments each path slot advances per k_step launch (0 = library default)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--kernel-timing", default="on", choices=["on", "off"],
                     help="HIP events around every extend/shade launch of the timed steps (roofline)")
@@ -112,7 +114,8 @@ def main():
     counts = [sum(t[2] * t[3] for t in ts) for ts in all_tiles]
     maxpix = max(counts)
     out = torch.zeros((maxpix, 3), dtype=tdtype, device=dev)
-    params = ctx.params(spp, depth, args.seed, prec, samples_per_item=args.chunk, pool_slots=args.pool)
+    params = ctx.params(spp, depth, args.seed, prec, samples_per_item=args.chunk, pool_slots=args.pool,
+                        segments_per_launch=args.segments_per_launch)
     fb = gathered = scatter_idx = None
     if rank == 0:
         fb = torch.zeros((H * W, 3), dtype=tdtype, device=dev)
@@ -135,7 +138,7 @@ def main():
         step()
     ctx.set_timing(args.kernel_timing == "on")
     ctx.reset_counters()
-    ext_ms = sh_ms = 0.0
+    step_ms = 0.0
     iters = 0
     if world > 1:
         dist.barrier()
@@ -144,8 +147,7 @@ def main():
     for _ in range(args.steps):
         step()
         st = ctx.stats()
-        ext_ms += st.extend_ms
-        sh_ms += st.shade_ms
+        step_ms += st.step_ms
         iters += st.iterations
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -168,19 +170,18 @@ def main():
     if rank == 0:
         my_samples = counts[0] * spp * args.steps
         seg_per_sample = segs / max(1, my_samples)
-        # dominant kernel of rank 0: per-launch algorithmic bytes / average launch duration (HIP events)
+        # dominant kernel of rank 0 (k_step: the fused extend+shade wavefront step): algorithmic bytes of
+        # SURVEY.md §8(d) per launch / average launch duration from HIP events on the render stream
         roof = None
         if args.kernel_timing == "on" and iters > 0:
-            kern, ms, bpseg = ("shade", sh_ms, B_SHADE) if sh_ms >= ext_ms else ("extend", ext_ms, B_EXT)
-            avg_s = ms / 1e3 / iters
-            bytes_per_launch = bpseg * segs / iters
-            achieved = bytes_per_launch / avg_s / 1e9
-            roof = {"bound": "hbm", "kernel": f"k_{kern}", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            alg_bytes = (B_GEN + B_ACC) * my_samples + (B_EXT + B_SHADE) * segs
+            avg_s = step_ms / 1e3 / iters
+            achieved = alg_bytes / (step_ms / 1e3) / 1e9
+            roof = {"bound": "hbm", "kernel": "k_step", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                     "avg_launch_us": round(avg_s * 1e6, 2), "launches": iters,
-                    "alg_bytes_per_launch": int(bytes_per_launch),
-                    "whole_job_alg_GBs": round((B_GEN + B_ACC + (B_EXT + B_SHADE) * seg_per_sample) *
-                                               my_samples / elapsed / 1e9, 1)}
+                    "alg_bytes_per_launch": int(alg_bytes / iters),
+                    "kernel_share_of_wall": round(step_ms / 1e3 / elapsed, 4)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(scene_name, width, aspect, spp, depth, args.seed, args.cpu_threads)

@@ -6,10 +6,10 @@
 //
 //   k_init    first camera ray of every slot            (camera.h:244-251)
 //   repeat:
-//     k_extend  closest hit of every live ray            (camera.h:198, world.hit)
-//     k_shade   emission + scatter + mixture pdf, or     (camera.h:199-240)
-//               finish the sample and regenerate the next camera ray of the
-//               slot's work item (pixel, chunk of samples)
+//     k_step    every live slot advances up to K segments: closest hit
+//               (camera.h:198, world.hit), then emission + scatter + mixture
+//               pdf (camera.h:199-240), or finish the sample and regenerate the
+//               next camera ray of the slot's work item (pixel, chunk of samples)
 //     every kBatch rounds: k_count/k_scan/k_compact build the live-slot queue
 //     (wave __ballot + block prefix sums) once half the pool has drained
 //   k_resolve  per-pixel mean over the chunks, in chunk order (camera.h:169-170)
@@ -40,32 +40,33 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kBatch = 16;           // extend/shade rounds between live-slot counts
 constexpr int kSegShards = 256;      // segment counter shards
-constexpr uint32_t kAutoPool32 = 1u << 20;
+constexpr uint32_t kAutoPool32 = 1u << 21;
 constexpr uint32_t kAutoPool64 = 1u << 19;
 constexpr uint32_t kAutoChunk = 16;
+constexpr int kAutoSegments = 16;  // segments each slot advances per k_step launch
 
 template <class R>
 struct alignas(4 * sizeof(R)) R4 {
   R x, y, z, w;
 };
-template <class R>
-struct alignas(16) HitRec {
-  R t;
-  uint32_t e;
-  int32_t i;
-};
 
+// Path state in HBM, one entry per slot, structure of arrays of 16-byte (fp32)
+// or 32-byte (fp64) records so every access is a coalesced dwordx4:
+//   O  origin, ray time            D  direction, bounce (-1: slot retired)
+//   T  throughput                  L  radiance of the running sample
+//   A  running sum of the item     S  key_pixel, key_sample, item, sample
+//   X  the surface the ray leaves (entry, instance): self-intersection exclusion
 template <class R>
 struct Params {
   DevScene<R> sc;
-  R4<R>* O;      // origin, time
-  R4<R>* D;      // direction, bounce (-1 = slot finished)
-  HitRec<R>* H;  // closest hit of the current segment / surface the ray leaves
-  R4<R>* T;      // path throughput
-  R4<R>* L;      // radiance of the current sample
-  R4<R>* A;      // sum of the finished samples of the current item
-  uint4* S;      // key_pixel, key_sample, item, sample (0-based within the pixel)
-  R* partial;    // per item: 3 sums
+  R4<R>* O;
+  R4<R>* D;
+  R4<R>* T;
+  R4<R>* L;
+  R4<R>* A;
+  uint4* S;
+  uint2* X;
+  R* partial;              // per item: 3 sums
   const uint32_t* pixmap;  // local pixel -> global pixel id y*W + x
   const uint32_t* queue;   // live slots, or null = slots [0, n)
   uint32_t n;
@@ -74,194 +75,136 @@ struct Params {
   uint64_t seed;
   V<R> pos, du, dv, dir00;
   unsigned long long* seg_shards;
-  bool feat_sph, feat_tri;  // scene has spheres / triangles (selects the linear kernel variant)
+  int32_t K;  // segments per launch
 };
 
-// ------------------------------------------------------------------ camera ray (camera.h:244-251,293)
 template <class R>
-__device__ __forceinline__ void camera_ray(const Params<R>& p, uint32_t gpix, Keys k, V<R>& o, V<R>& d, R& tm) {
-  uint32_t x = gpix % p.W, y = gpix / p.W;
-  V<R> rd = (p.dir00 + R(x) * p.du) + R(y) * p.dv;
-  R ox = to_unit<R>(draw_u32(k.ka, k.kb, 0)) - R(0.5);
-  R oy = to_unit<R>(draw_u32(k.ka, k.kb, 1)) - R(0.5);
-  d = (rd + ox * p.du) + oy * p.dv;
-  tm = to_unit<R>(draw_u32(k.ka, k.kb, 2));
-  o = p.pos;
+struct Path {
+  V<R> o, d, thr, rad, acc;
+  R tm;
+  int32_t bounce;
+  uint32_t ka, kb, item, sample;
+  uint32_t xe;
+  int32_t xi;
+};
+
+template <class R>
+__device__ __forceinline__ void load_path(const Params<R>& p, uint32_t slot, R4<R> Dv, Path<R>& s) {
+  R4<R> Ov = p.O[slot], Tv = p.T[slot], Lv = p.L[slot], Av = p.A[slot];
+  uint4 S = p.S[slot];
+  uint2 X = p.X[slot];
+  s.o = mkv(Ov.x, Ov.y, Ov.z);
+  s.tm = Ov.w;
+  s.d = mkv(Dv.x, Dv.y, Dv.z);
+  s.bounce = (int32_t)Dv.w;
+  s.thr = mkv(Tv.x, Tv.y, Tv.z);
+  s.rad = mkv(Lv.x, Lv.y, Lv.z);
+  s.acc = mkv(Av.x, Av.y, Av.z);
+  s.ka = S.x;
+  s.kb = S.y;
+  s.item = S.z;
+  s.sample = S.w;
+  s.xe = X.x;
+  s.xi = (int32_t)X.y;
 }
 
 template <class R>
-__device__ __forceinline__ void begin_sample(const Params<R>& p, uint32_t slot, uint32_t item, uint32_t sample,
-                                             R4<R> acc) {
+__device__ __forceinline__ void store_path(const Params<R>& p, uint32_t slot, const Path<R>& s) {
+  p.D[slot] = {s.d.x, s.d.y, s.d.z, R(s.bounce)};
+  if (s.bounce < 0) return;
+  p.O[slot] = {s.o.x, s.o.y, s.o.z, s.tm};
+  p.T[slot] = {s.thr.x, s.thr.y, s.thr.z, R(0)};
+  p.L[slot] = {s.rad.x, s.rad.y, s.rad.z, R(0)};
+  p.A[slot] = {s.acc.x, s.acc.y, s.acc.z, R(0)};
+  p.S[slot] = make_uint4(s.ka, s.kb, s.item, s.sample);
+  p.X[slot] = make_uint2(s.xe, (uint32_t)s.xi);
+}
+
+// camera::generate_ray, perspective mode (camera.h:244-251,293): a new sample of the slot's item
+template <class R>
+__device__ __forceinline__ void begin_sample(const Params<R>& p, Path<R>& s, uint32_t item, uint32_t sample) {
   uint32_t gpix = p.pixmap[item % p.npix];
-  Keys k{key_pixel(p.seed, gpix), key_sample(p.seed, p.first_sample + sample)};
-  V<R> o, d;
-  R tm;
-  camera_ray(p, gpix, k, o, d, tm);
-  p.O[slot] = {o.x, o.y, o.z, tm};
-  p.D[slot] = {d.x, d.y, d.z, R(0)};
-  p.T[slot] = {R(1), R(1), R(1), R(0)};
-  p.L[slot] = {R(0), R(0), R(0), R(0)};
-  p.A[slot] = acc;
-  p.S[slot] = make_uint4(k.ka, k.kb, item, sample);
-  HitRec<R> h;
-  h.t = R(0);
-  h.e = kNoHit;
-  h.i = -1;
-  p.H[slot] = h;
+  s.item = item;
+  s.sample = sample;
+  s.ka = key_pixel(p.seed, gpix);
+  s.kb = key_sample(p.seed, p.first_sample + sample);
+  uint32_t x = gpix % p.W, y = gpix / p.W;
+  V<R> rd = (p.dir00 + R(x) * p.du) + R(y) * p.dv;
+  R ox = to_unit<R>(draw_u32(s.ka, s.kb, 0)) - R(0.5);
+  R oy = to_unit<R>(draw_u32(s.ka, s.kb, 1)) - R(0.5);
+  s.d = (rd + ox * p.du) + oy * p.dv;
+  s.tm = to_unit<R>(draw_u32(s.ka, s.kb, 2));
+  s.o = p.pos;
+  s.bounce = 0;
+  s.thr = mkv(R(1), R(1), R(1));
+  s.rad = mkv(R(0), R(0), R(0));
+  s.xe = kNoHit;
+  s.xi = -1;
 }
 
 template <class R>
 __global__ __launch_bounds__(kBlock) void k_init(Params<R> p) {
   uint32_t slot = blockIdx.x * kBlock + threadIdx.x;
   if (slot >= p.P) return;
+  Path<R> s;
+  s.acc = mkv(R(0), R(0), R(0));
   if (slot >= p.n_items) {
-    p.D[slot] = {R(0), R(0), R(0), R(-1)};
-    return;
+    s.d = mkv(R(0), R(0), R(0));
+    s.bounce = -1;
+  } else {
+    begin_sample(p, s, slot, (slot / p.npix) * p.chunk);
   }
-  uint32_t item = slot;
-  begin_sample(p, slot, item, (item / p.npix) * p.chunk, R4<R>{R(0), R(0), R(0), R(0)});
+  store_path(p, slot, s);
 }
 
-// ------------------------------------------------------------------ extend
-template <class R, int STACK>
-__global__ __launch_bounds__(kBlock) void k_extend(Params<R> p) {
-  __shared__ uint32_t stk[STACK * kBlock];
-  __shared__ uint32_t wave_cnt[kBlock / 64];
-  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  bool active = i < p.n;
-  uint32_t slot = 0;
-  R4<R> Dv{};
-  if (active) {
-    slot = p.queue ? p.queue[i] : i;
-    Dv = p.D[slot];
-    active = Dv.w >= R(0);
-  }
-  if (active) {
-    R4<R> Ov = p.O[slot];
-    HitRec<R> prev = p.H[slot];
-    Keys k{0, 0};
-    if (p.sc.has_volumes) {
-      uint4 s = p.S[slot];
-      k = {s.x, s.y};
-    }
-    R t;
-    uint32_t e;
-    int32_t inst;
-    trace<R, STACK, kBlock>(p.sc, mkv(Ov.x, Ov.y, Ov.z), mkv(Dv.x, Dv.y, Dv.z), Ov.w, prev.e, prev.i, k,
-                            (uint32_t)Dv.w, stk + threadIdx.x, t, e, inst);
-    HitRec<R> h;
-    h.t = t;
-    h.e = e;
-    h.i = inst;
-    p.H[slot] = h;
-  }
-  // segments traced: one count per wave, one atomic per block
-  unsigned long long m = __ballot(active);
-  int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) wave_cnt[wave] = (uint32_t)__popcll(m);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t c = 0;
-    for (int w = 0; w < kBlock / 64; w++) c += wave_cnt[w];
-    if (c) atomicAdd(&p.seg_shards[blockIdx.x % kSegShards], (unsigned long long)c);
-  }
-}
-
-template <class R, bool SPH, bool TRI, bool VOL>
-__global__ __launch_bounds__(kBlock) void k_extend_linear(Params<R> p) {
-  __shared__ uint32_t wave_cnt[kBlock / 64];
-  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  bool active = i < p.n;
-  uint32_t slot = 0;
-  R4<R> Dv{};
-  if (active) {
-    slot = p.queue ? p.queue[i] : i;
-    Dv = p.D[slot];
-    active = Dv.w >= R(0);
-  }
-  if (active) {
-    R4<R> Ov = p.O[slot];
-    HitRec<R> prev = p.H[slot];
-    Keys k{0, 0};
-    if (VOL) {
-      uint4 s = p.S[slot];
-      k = {s.x, s.y};
-    }
-    HitRec<R> h;
-    trace_linear<R, SPH, TRI, VOL>(p.sc, mkv(Ov.x, Ov.y, Ov.z), mkv(Dv.x, Dv.y, Dv.z), Ov.w, prev.e, prev.i, k,
-                                   (uint32_t)Dv.w, h.t, h.e, h.i);
-    p.H[slot] = h;
-  }
-  unsigned long long m = __ballot(active);
-  int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) wave_cnt[wave] = (uint32_t)__popcll(m);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t c = 0;
-    for (int w = 0; w < kBlock / 64; w++) c += wave_cnt[w];
-    if (c) atomicAdd(&p.seg_shards[blockIdx.x % kSegShards], (unsigned long long)c);
-  }
-}
-
-// ------------------------------------------------------------------ shade
+// camera::ray_color for one segment (camera.h:193-241), iteratively: given the
+// closest hit (t, e, inst) of s's ray, add emission, scatter (or finish the
+// sample and regenerate the slot's next camera ray). Returns false once the slot
+// has no work left.
 template <class R>
-__global__ __launch_bounds__(kBlock) void k_shade(Params<R> p) {
-  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= p.n) return;
-  uint32_t slot = p.queue ? p.queue[i] : i;
-  R4<R> Dv = p.D[slot];
-  if (Dv.w < R(0)) return;
+__device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t inst) {
   const DevScene<R>& sc = p.sc;
-  R4<R> Ov = p.O[slot];
-  HitRec<R> h = p.H[slot];
-  R4<R> Tv = p.T[slot];
-  uint4 S = p.S[slot];
-  Keys k{S.x, S.y};
-  uint32_t bounce = (uint32_t)Dv.w;
-  V<R> o = mkv(Ov.x, Ov.y, Ov.z), d = mkv(Dv.x, Dv.y, Dv.z);
-  R tm = Ov.w;
-  V<R> thr = mkv(Tv.x, Tv.y, Tv.z);
   V<R> add = mkv(R(0), R(0), R(0));
   bool has_add = false, done = false;
-  V<R> new_o = o, new_d = d;
+  V<R> new_o = s.o, new_d = s.d;
+  const V<R> o = s.o, d = s.d;
 
-  if (h.e == kNoHit) {  // camera::miss (camera.h:180-190)
+  if (e == kNoHit) {  // camera::miss (camera.h:180-190)
     if (sc.background >= 0) {
-      R t;
-      if (sphere_roots<R>(o.x, o.y, o.z, d.x, d.y, d.z, o.x, o.y, o.z, R(1), R(0.001), Num<R>::inf(), false, t)) {
-        V<R> ph = o + t * d;
-        add = thr * tex_sample(sc.texs[sc.background], ph);
+      R tb;
+      if (sphere_roots<R>(o.x, o.y, o.z, d.x, d.y, d.z, o.x, o.y, o.z, R(1), R(0.001), Num<R>::inf(), false, tb)) {
+        add = s.thr * tex_sample(sc.texs[sc.background], o + tb * d);
         has_add = true;
       }
     }
     done = true;
   } else {
-    uint32_t ty = etype(h.e), idx = epay(h.e);
+    uint32_t ty = etype(e), idx = epay(e);
     V<R> pw, n;
     bool front;
     int32_t mat;
     if (ty == E_VOLUME) {  // volumne.h:40-44
-      pw = o + h.t * d;
+      pw = o + t * d;
       n = mkv(R(1), R(0), R(0));
       front = true;
       mat = sc.vols[idx].phase_mat;
     } else {
       V<R> oo = o, dd = d;
       const Instance<R>* in = nullptr;
-      if (h.i >= 0) {
-        in = &sc.insts[h.i];
+      if (inst >= 0) {
+        in = &sc.insts[inst];
         chain_in(*in, oo, dd);
       }
-      V<R> po = oo + h.t * dd;
+      V<R> po = oo + t * dd;
       V<R> outward;
       if (ty == E_QUAD) {
         const Quad<R>& q = sc.quads[idx];
         outward = ld3(q.n);
         mat = q.mat;
       } else if (ty == E_SPHERE) {  // sphere.h:69 (center_ member; (0,0,0) for moving spheres)
-        const Sphere<R>& s = sc.spheres[idx];
-        outward = (po - ld3(s.cn)) / s.r;
-        mat = s.mat;
+        const Sphere<R>& sp = sc.spheres[idx];
+        outward = (po - ld3(sp.cn)) / sp.r;
+        mat = sp.mat;
       } else {
         const Tri<R>& tr = sc.tris[idx];
         outward = ld3(tr.n);
@@ -280,20 +223,21 @@ __global__ __launch_bounds__(kBlock) void k_shade(Params<R> p) {
     const Material<R>& m = sc.mats[mat];
     if (m.kind == M_DIFFUSE_LIGHT) {  // material.h:211-215; no scatter
       if (front) {
-        add = thr * tex_sample(sc.texs[m.tex], pw);
+        add = s.thr * tex_sample(sc.texs[m.tex], pw);
         has_add = true;
       }
       done = true;
     } else {
       V<R> att = tex_sample(sc.texs[m.tex], pw);
+      const uint32_t bounce = (uint32_t)s.bounce;
       uint32_t js = 0;
-      auto U = [&]() { return to_unit<R>(draw_u32(k.ka, k.kb, dim_scatter(bounce, js++))); };
+      auto U = [&]() { return to_unit<R>(draw_u32(s.ka, s.kb, dim_scatter(bounce, js++))); };
       if (m.kind == M_METAL) {  // material.h:85-92
         V<R> dir = unit(reflect(d, n));
         R u1 = U();
         R u2 = U();
         new_d = dir + m.fuzz * unit(on_sphere(u1, u2));
-        thr = thr * att;
+        s.thr = s.thr * att;
       } else if (m.kind == M_DIELECTRIC) {  // material.h:113-131
         R ri = front ? (R(1) / m.refr) : m.refr;
         V<R> ud = unit(d);
@@ -306,17 +250,16 @@ __global__ __launch_bounds__(kBlock) void k_shade(Params<R> p) {
           new_d = reflect(ud, n);
         else
           new_d = refract(ud, n, ri);
-        thr = thr * att;
+        s.thr = s.thr * att;
       } else {  // lambertian (material.h:62-72) / isotropic (material.h:193-200): kRandom
         const bool iso = m.kind == M_ISOTROPIC;
-        const R inv_pi = R(1) / Num<R>::pi();
         const R iso_pdf = R(1) / (R(4) * Num<R>::pi());
         Onb<R> b;
         if (!iso) b = make_onb(n);
-        const Light<R>& L = *sc.light;
+        const Light<R>& Lt = *sc.light;
         R pv;
         V<R> dir;
-        if (L.kind == L_NONE) {  // camera.h:217-226
+        if (Lt.kind == L_NONE) {  // camera.h:217-226
           R u1 = U();
           R u2 = U();
           dir = iso ? unit(on_sphere(u1, u2)) : onb_transform(b, cosine_dir(u1, u2));
@@ -326,61 +269,122 @@ __global__ __launch_bounds__(kBlock) void k_shade(Params<R> p) {
           R u1 = U();
           R u2 = U();
           if (c < R(0.5))
-            dir = light_random(L, pw, u1, u2);
+            dir = light_random(Lt, pw, u1, u2);
           else
             dir = iso ? unit(on_sphere(u1, u2)) : onb_transform(b, cosine_dir(u1, u2));
           R mp = iso ? iso_pdf : fmax(R(0), dot(unit(dir), b.y) / Num<R>::pi());
-          pv = R(0.5) * light_pdf(L, pw, dir) + R(0.5) * mp;
+          pv = R(0.5) * light_pdf(Lt, pw, dir) + R(0.5) * mp;
         }
         R ps;
         if (iso) {
           ps = iso_pdf;
         } else {
           R c = dot(n, unit(dir));
-          ps = c < R(0) ? R(0) : c * inv_pi;
+          ps = c < R(0) ? R(0) : c / Num<R>::pi();
         }
-        (void)inv_pi;
-        thr = thr * ((att * ps) / pv);
+        s.thr = s.thr * ((att * ps) / pv);
         new_d = dir;
       }
       new_o = pw;
-      if ((int32_t)bounce + 1 >= p.max_depth) done = true;  // ray_color(.., 0) returns 0
-      if (thr.x == R(0) && thr.y == R(0) && thr.z == R(0)) done = true;
+      if (s.bounce + 1 >= p.max_depth) done = true;  // ray_color(.., 0) returns 0 (camera.h:194)
+      if (s.thr.x == R(0) && s.thr.y == R(0) && s.thr.z == R(0)) done = true;
     }
   }
-
+  if (has_add) s.rad = s.rad + add;
   if (!done) {
-    if (has_add) {
-      R4<R> Lv = p.L[slot];
-      p.L[slot] = {Lv.x + add.x, Lv.y + add.y, Lv.z + add.z, R(0)};
-    }
-    p.O[slot] = {new_o.x, new_o.y, new_o.z, tm};
-    p.D[slot] = {new_d.x, new_d.y, new_d.z, R(bounce + 1)};
-    p.T[slot] = {thr.x, thr.y, thr.z, R(0)};
-    return;
+    s.o = new_o;
+    s.d = new_d;
+    s.bounce += 1;
+    s.xe = e;
+    s.xi = inst;
+    return true;
   }
-  // finish the sample (camera.h:167): add its radiance to the item's running sum
-  R4<R> Lv = p.L[slot];
-  R4<R> Av = p.A[slot];
-  V<R> rad = mkv(Lv.x, Lv.y, Lv.z);
-  if (has_add) rad = rad + add;
-  R4<R> acc{Av.x + rad.x, Av.y + rad.y, Av.z + rad.z, R(0)};
-  uint32_t item = S.z, sample = S.w + 1;
+  // the sample is finished (camera.h:167): add it to the item's running sum
+  s.acc = s.acc + s.rad;
+  uint32_t item = s.item, sample = s.sample + 1;
   uint32_t chunk_end = min((item / p.npix) * p.chunk + p.chunk, p.spp);
   if (sample >= chunk_end) {
     R* dst = p.partial + 3ull * item;
-    dst[0] = acc.x;
-    dst[1] = acc.y;
-    dst[2] = acc.z;
-    acc = {R(0), R(0), R(0), R(0)};
+    dst[0] = s.acc.x;
+    dst[1] = s.acc.y;
+    dst[2] = s.acc.z;
+    s.acc = mkv(R(0), R(0), R(0));
     item += p.P;
     if (item >= p.n_items) {
-      p.D[slot] = {R(0), R(0), R(0), R(-1)};
-      return;
+      s.bounce = -1;
+      return false;
     }
     sample = (item / p.npix) * p.chunk;
   }
-  begin_sample(p, slot, item, sample, acc);
+  begin_sample(p, s, item, sample);
+  return true;
+}
+
+// ------------------------------------------------------------------ the fused wavefront step
+// Each launch advances every live slot by up to K segments: closest hit
+// (extend, camera.h:198), then shade. Traversal: the wave-uniform linear
+// program (small scenes) or the BVH stack machine with a per-lane LDS stack.
+template <class R, bool SPH, bool TRI, bool VOL>
+struct LinearTrav {
+  static constexpr int kStack = 0;
+  __device__ __forceinline__ static void run(const DevScene<R>& sc, const Path<R>& s, Keys k, uint32_t*, R& t,
+                                             uint32_t& e, int32_t& i) {
+    trace_linear<R, SPH, TRI, VOL>(sc, s.o, s.d, s.tm, s.xe, s.xi, k, (uint32_t)s.bounce, t, e, i);
+  }
+};
+template <class R, int STACK>
+struct StackTrav {
+  static constexpr int kStack = STACK;
+  __device__ __forceinline__ static void run(const DevScene<R>& sc, const Path<R>& s, Keys k, uint32_t* stk, R& t,
+                                             uint32_t& e, int32_t& i) {
+    trace<R, STACK, kBlock>(sc, s.o, s.d, s.tm, s.xe, s.xi, k, (uint32_t)s.bounce, stk, t, e, i);
+  }
+};
+
+template <int N>
+struct Lds {
+  uint32_t v[N];
+};
+template <>
+struct Lds<0> {
+  uint32_t v[1];
+};
+
+template <class R, class Trav>
+__global__ __launch_bounds__(kBlock) void k_step(Params<R> p) {
+  __shared__ Lds<Trav::kStack * kBlock> stk;
+  __shared__ uint32_t wave_cnt[kBlock / 64];
+  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  uint32_t slot = 0, segs = 0;
+  bool active = i < p.n;
+  R4<R> Dv{};
+  if (active) {
+    slot = p.queue ? p.queue[i] : i;
+    Dv = p.D[slot];
+    active = Dv.w >= R(0);
+  }
+  if (active) {
+    Path<R> s;
+    load_path(p, slot, Dv, s);
+#pragma unroll 1
+    for (int k = 0; k < p.K; k++) {
+      R t;
+      uint32_t e;
+      int32_t inst;
+      Trav::run(p.sc, s, Keys{s.ka, s.kb}, stk.v + threadIdx.x, t, e, inst);
+      segs++;
+      if (!shade(p, s, t, e, inst)) break;
+    }
+    store_path(p, slot, s);
+  }
+  // segments traced: wave sums, one atomic per block
+  for (int off = 32; off > 0; off >>= 1) segs += __shfl_xor(segs, off);
+  if ((threadIdx.x & 63) == 0) wave_cnt[threadIdx.x >> 6] = segs;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t c = wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3];
+    if (c) atomicAdd(&p.seg_shards[blockIdx.x % kSegShards], (unsigned long long)c);
+  }
 }
 
 // ------------------------------------------------------------------ live-slot compaction
@@ -595,28 +599,30 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
   return s;
 }
 
+template <class R, class Trav>
+void launch_k(const Params<R>& p, uint32_t grid, hipStream_t st) {
+  hipLaunchKernelGGL((k_step<R, Trav>), dim3(grid), dim3(kBlock), 0, st, p);
+}
+
 template <class R>
-void launch_extend2(const Params<R>& p, int stack, uint32_t grid, hipStream_t st) {
+void launch_step(const Params<R>& p, int stack, bool sph, bool tri, uint32_t grid, hipStream_t st) {
+  const bool vol = p.sc.has_volumes != 0;
   if (p.sc.n_linear > 0) {
-    const bool sph = p.feat_sph, tri = p.feat_tri, vol = p.sc.has_volumes != 0;
-#define RT_LIN(S, T, V) hipLaunchKernelGGL((k_extend_linear<R, S, T, V>), dim3(grid), dim3(kBlock), 0, st, p)
     if (!sph && !tri && !vol)
-      RT_LIN(false, false, false);
+      launch_k<R, LinearTrav<R, false, false, false>>(p, grid, st);
     else if (!sph && !tri && vol)
-      RT_LIN(false, false, true);
+      launch_k<R, LinearTrav<R, false, false, true>>(p, grid, st);
     else if (sph && !tri && !vol)
-      RT_LIN(true, false, false);
+      launch_k<R, LinearTrav<R, true, false, false>>(p, grid, st);
     else
-      RT_LIN(true, true, true);
-#undef RT_LIN
-    return;
+      launch_k<R, LinearTrav<R, true, true, true>>(p, grid, st);
+  } else if (stack <= 8) {
+    launch_k<R, StackTrav<R, 8>>(p, grid, st);
+  } else if (stack <= 16) {
+    launch_k<R, StackTrav<R, 16>>(p, grid, st);
+  } else {
+    launch_k<R, StackTrav<R, kStackDepth>>(p, grid, st);
   }
-  if (stack <= 8)
-    hipLaunchKernelGGL((k_extend<R, 8>), dim3(grid), dim3(kBlock), 0, st, p);
-  else if (stack <= 16)
-    hipLaunchKernelGGL((k_extend<R, 16>), dim3(grid), dim3(kBlock), 0, st, p);
-  else
-    hipLaunchKernelGGL((k_extend<R, kStackDepth>), dim3(grid), dim3(kBlock), 0, st, p);
 }
 
 template <class R>
@@ -660,10 +666,10 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     P = std::max<uint32_t>(1, std::min(P, n_items));
     const uint32_t nblk_max = (P + kBlock - 1) / kBlock;
 
-    // path state: 5 R4 arrays + hit records + uint4 keys, each P long
+    // path state: 5 R4 arrays (O, D, T, L, A) + uint4 keys (S) + uint2 exclusion (X), each P long
     auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
-    const size_t r4 = al(sizeof(R4<R>) * (size_t)P), hb = al(sizeof(HitRec<R>) * (size_t)P), sb = al(16 * (size_t)P);
-    if ((s = ensure(c, c->state, 5 * r4 + hb + sb)) != RT_OK) return s;
+    const size_t r4 = al(sizeof(R4<R>) * (size_t)P), sb = al(16 * (size_t)P), xb = al(8 * (size_t)P);
+    if ((s = ensure(c, c->state, 5 * r4 + sb + xb)) != RT_OK) return s;
     if ((s = ensure(c, c->partial, 3ull * n_items * sizeof(R))) != RT_OK) return s;
     if ((s = ensure(c, c->pixmap, 4ull * npix)) != RT_OK) return s;
     if ((s = ensure(c, c->queue0, 4ull * P)) != RT_OK) return s;
@@ -680,8 +686,8 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     p.T = (R4<R>*)(sp + 2 * r4);
     p.L = (R4<R>*)(sp + 3 * r4);
     p.A = (R4<R>*)(sp + 4 * r4);
-    p.H = (HitRec<R>*)(sp + 5 * r4);
-    p.S = (uint4*)(sp + 5 * r4 + hb);
+    p.S = (uint4*)(sp + 5 * r4);
+    p.X = (uint2*)(sp + 5 * r4 + sb);
     p.partial = (R*)c->partial.ptr;
     p.pixmap = (const uint32_t*)c->pixmap.ptr;
     p.queue = nullptr;
@@ -701,8 +707,8 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     p.dv = tov<R>(vw.dv);
     p.dir00 = tov<R>(vw.dir00);
     p.seg_shards = (unsigned long long*)c->counters.ptr;
-    p.feat_sph = hdr.n_spheres > 0;
-    p.feat_tri = hdr.n_tris > 0;
+    const int K = prm->segments_per_launch > 0 ? std::min(prm->segments_per_launch, 64) : kAutoSegments;
+    p.K = K;
 
     hipLaunchKernelGGL(k_init<R>, dim3(nblk_max), dim3(kBlock), 0, st, p);
     uint64_t launches = 1, iters = 0;
@@ -711,30 +717,24 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     uint32_t* blk = (uint32_t*)c->blk.ptr;
     uint32_t* d_total = blk + nblk_max + 1;
     size_t ev = 0;
-    std::vector<std::pair<int, size_t>> timed;  // (0 extend / 1 shade, event index)
-    // every slot finishes within (items per slot) * chunk * max_depth rounds; anything longer is a bug
-    const uint64_t iter_cap = ((uint64_t)(n_items + P - 1) / P) * chunk * (uint64_t)prm->max_depth + 4 * kBatch;
+    // every slot finishes within (items per slot) * chunk * max_depth segments; anything longer is a bug
+    const uint64_t iter_cap =
+        (((uint64_t)(n_items + P - 1) / P) * chunk * (uint64_t)prm->max_depth + K - 1) / K + 4 * kBatch;
     for (;;) {
       if (iters > iter_cap) return set_err(c, RT_ERR_HIP, "wavefront did not drain (internal error)");
       const uint32_t grid = (p.n + kBlock - 1) / kBlock;
       for (int b = 0; b < kBatch; b++) {
-        hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
         if (c->timing) {
-          e0 = take_event(c, ev);
-          e1 = take_event(c, ev + 1);
-          e2 = take_event(c, ev + 2);
-          if (!e0 || !e1 || !e2) return set_err(c, RT_ERR_HIP, "hipEventCreate failed");
+          hipEvent_t e0 = take_event(c, ev), e1 = take_event(c, ev + 1);
+          if (!e0 || !e1) return set_err(c, RT_ERR_HIP, "hipEventCreate failed");
           RT_HIP(c, hipEventRecord(e0, st));
+          launch_step<R>(p, cs.stack_need, hdr.n_spheres > 0, hdr.n_tris > 0, grid, st);
+          RT_HIP(c, hipEventRecord(e1, st));
+          ev += 2;
+        } else {
+          launch_step<R>(p, cs.stack_need, hdr.n_spheres > 0, hdr.n_tris > 0, grid, st);
         }
-        launch_extend2<R>(p, cs.stack_need, grid, st);
-        if (c->timing) RT_HIP(c, hipEventRecord(e1, st));
-        hipLaunchKernelGGL(k_shade<R>, dim3(grid), dim3(kBlock), 0, st, p);
-        if (c->timing) {
-          RT_HIP(c, hipEventRecord(e2, st));
-          timed.push_back({0, ev});
-          ev += 3;
-        }
-        launches += 2;
+        launches++;
         iters++;
       }
       RT_HIP(c, hipGetLastError());
@@ -771,16 +771,13 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     last.iterations = iters;
     last.launches = launches;
     if (c->timing) {
-      double ext = 0, sh = 0;
-      for (auto& t : timed) {
-        float a = 0, b = 0;
-        RT_HIP(c, hipEventElapsedTime(&a, c->events[t.second], c->events[t.second + 1]));
-        RT_HIP(c, hipEventElapsedTime(&b, c->events[t.second + 1], c->events[t.second + 2]));
-        ext += a;
-        sh += b;
+      double ms = 0;
+      for (size_t k = 0; k + 1 < ev; k += 2) {
+        float a = 0;
+        RT_HIP(c, hipEventElapsedTime(&a, c->events[k], c->events[k + 1]));
+        ms += a;
       }
-      last.extend_ms = ext;
-      last.shade_ms = sh;
+      last.step_ms = ms;
     }
   }
   if (!out_dev) {

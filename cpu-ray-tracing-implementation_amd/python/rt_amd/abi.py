@@ -59,7 +59,8 @@ class rt_camera_desc(ctypes.Structure):
 
 class rt_render_params(ctypes.Structure):
     _fields_ = [("spp", c_int32), ("max_depth", c_int32), ("seed", c_uint64), ("precision", c_int32),
-                ("first_sample", c_int32), ("samples_per_item", c_int32), ("pool_slots", c_int32)]
+                ("first_sample", c_int32), ("samples_per_item", c_int32), ("pool_slots", c_int32),
+                ("segments_per_launch", c_int32), ("pad_", c_int32)]
 
 
 class rt_tile(ctypes.Structure):
@@ -68,7 +69,7 @@ class rt_tile(ctypes.Structure):
 
 class rt_counters(ctypes.Structure):
     _fields_ = [("segments", c_uint64), ("samples", c_uint64), ("iterations", c_uint64), ("launches", c_uint64),
-                ("last_render_ms", c_double), ("extend_ms", c_double), ("shade_ms", c_double)]
+                ("last_render_ms", c_double), ("step_ms", c_double), ("aux_ms", c_double)]
 
 
 # every symbol include/rt_hip.h declares, with its ctypes signature

@@ -166,6 +166,9 @@ typedef struct rt_render_params {
   int32_t first_sample;     /* render samples [first_sample, first_sample + spp) of each pixel */
   int32_t samples_per_item; /* samples one work item accumulates (0 = auto). Does not change the image. */
   int32_t pool_slots;       /* wavefront pool size (0 = auto). Does not change the image. */
+  int32_t segments_per_launch; /* segments each path slot advances per kernel launch (0 = auto).
+                                  Does not change the image. */
+  int32_t pad_;
 } rt_render_params;
 
 /* A framebuffer rectangle. Output of a render call is the tiles packed in the
@@ -186,8 +189,8 @@ typedef struct rt_counters {
   uint64_t iterations; /* extend/shade rounds of the last render */
   uint64_t launches;   /* kernel launches of the last render */
   double last_render_ms;
-  double extend_ms; /* device time of the extend kernels (last render, when timing enabled) */
-  double shade_ms;  /* device time of the shade kernels (last render, when timing enabled) */
+  double step_ms; /* device time of the path-step kernels (last render, when timing is enabled) */
+  double aux_ms;  /* reserved */
 } rt_counters;
 
 typedef struct rt_context rt_context;
