@@ -9,11 +9,23 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC -Wall --offload-arch=$(ARCH)
 LIB_SRCS := $(PKG)/csrc/rt_kernels.hip $(PKG)/csrc/scene_compile.cpp
 LIB_HDRS := $(PKG)/csrc/rt_device.h $(PKG)/csrc/rt_scene.h $(PKG)/csrc/scene_compile.h include/rt_hip.h
 
-all: $(BUILD)/librt_hip.so oracle
+CXX      ?= g++
+CXXFLAGS ?= -O2 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter
+RT_HDRS  := $(wildcard $(PKG)/rt/*.h) include/rt_hip.h
+
+all: $(BUILD)/librt_hip.so $(BUILD)/librt_scenes.so $(BUILD)/rt_main oracle
 
 $(BUILD)/librt_hip.so: $(LIB_SRCS) $(LIB_HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(LIB_SRCS)
+
+# the reference's config scenes written against the drop-in plugin surface (+ rtsc_* C ABI for tests)
+$(BUILD)/librt_scenes.so: $(PKG)/scenes/config_scenes.cpp $(PKG)/scenes/config_scenes.h $(RT_HDRS) $(BUILD)/librt_hip.so
+	$(CXX) $(CXXFLAGS) -shared -o $@ $(PKG)/scenes/config_scenes.cpp -L$(BUILD) -lrt_hip -Wl,-rpath,'$$ORIGIN'
+
+# the reference's main.cc driver on the plugin surface
+$(BUILD)/rt_main: examples/main.cc $(PKG)/scenes/config_scenes.cpp $(PKG)/scenes/config_scenes.h $(RT_HDRS) $(BUILD)/librt_hip.so
+	$(CXX) $(CXXFLAGS) -o $@ examples/main.cc $(PKG)/scenes/config_scenes.cpp -L$(BUILD) -lrt_hip -Wl,-rpath,'$$ORIGIN'
 
 oracle:
 	$(MAKE) -C oracle

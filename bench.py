@@ -12,7 +12,6 @@ gathers them (RCCL, torch.distributed "nccl") into the full linear framebuffer.
 """
 import argparse
 import json
-import math
 import os
 import sys
 import time
@@ -25,7 +24,8 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import rt_amd  # noqa: E402
-from rt_amd import abi, scenes  # noqa: E402
+from rt_amd import abi, plugin  # noqa: E402
+from rt_amd.tiling import pixel_index, plan  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 # SURVEY.md §8(d) algorithmic bytes: per sample (generate + finalise) and per segment
@@ -40,25 +40,13 @@ CONFIGS = {
 }
 
 
-def tiles_of(w, h, rank, world, ts=64):
-    all_tiles = [(x, y, min(ts, w - x), min(ts, h - y)) for y in range(0, h, ts) for x in range(0, w, ts)]
-    return all_tiles[rank::world]
-
-
-def pixel_index(tiles, w):
-    idx = []
-    for (x0, y0, tw, th) in tiles:
-        ys, xs = np.mgrid[y0:y0 + th, x0:x0 + tw]
-        idx.append((ys * w + xs).reshape(-1))
-    return np.concatenate(idx) if idx else np.zeros(0, dtype=np.int64)
-
-
 def cpu_baseline(scene_name, width, aspect, spp, depth, seed, threads):
     """The oracle (fp64 restatement of the reference loop) on host cores, over a row sample."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
-    desc, cam, _, _ = scenes.SCENES[scene_name](width=width, aspect=aspect)
-    osc = oracle.from_desc(desc)
+    cs = plugin.ConfigScene(scene_name, width, aspect)
+    cam = cs.cam
+    osc = oracle.from_desc(cs.desc)
     # about 80 Msamples (a few seconds on 16 cores): evenly spaced full rows at the full spp and depth
     nrows = max(1, min(cam.image_height, int(80e6 // (cam.image_width * spp))))
     step = cam.image_height // nrows
@@ -102,17 +90,17 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     scene_name, width, aspect, spp, depth = CONFIGS[args.config]
-    desc, cam, _, _ = scenes.SCENES[scene_name](width=width, aspect=aspect)
+    # the scene exactly as the drop-in camera::render flattens it (C++ plugin surface, main.cc:198-225)
+    cs = plugin.ConfigScene(scene_name, width, aspect)
+    cam = cs.cam
     W, H = cam.image_width, cam.image_height
     prec = abi.RT_PREC_F64 if args.precision == "f64" else abi.RT_PREC_F32
     tdtype = torch.float64 if prec == abi.RT_PREC_F64 else torch.float32
 
     ctx = rt_amd.Context(local)
-    ctx.upload(desc)
-    my_tiles = tiles_of(W, H, rank, world)
-    all_tiles = [tiles_of(W, H, r, world) for r in range(world)]
-    counts = [sum(t[2] * t[3] for t in ts) for ts in all_tiles]
-    maxpix = max(counts)
+    ctx.upload(cs.desc)
+    all_tiles, counts, maxpix = plan(W, H, world)
+    my_tiles = all_tiles[rank]
     out = torch.zeros((maxpix, 3), dtype=tdtype, device=dev)
     params = ctx.params(spp, depth, args.seed, prec, samples_per_item=args.chunk, pool_slots=args.pool,
                         segments_per_launch=args.segments_per_launch)

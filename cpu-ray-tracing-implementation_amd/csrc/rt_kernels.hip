@@ -26,6 +26,8 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <new>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -867,6 +869,28 @@ rt_status rt_scene_upload(rt_context* c, const rt_scene_desc* desc) {
   return RT_OK;
 }
 
+rt_status rt_scene_check(const rt_scene_desc* desc, rt_scene_info* info, char* err, int32_t errlen) {
+  CompiledScene cs;
+  std::string m;
+  rt_status s = desc ? compile_scene(desc, &cs, &m) : RT_ERR_INVALID_ARGUMENT;
+  if (!desc) m = "null descriptor";
+  if (err && errlen > 0) std::snprintf(err, (size_t)errlen, "%s", m.c_str());
+  if (s == RT_OK && info) {
+    const SceneHeader& h = cs.hdr;
+    info->quads = (int32_t)h.n_quads;
+    info->spheres = (int32_t)h.n_spheres;
+    info->triangles = (int32_t)h.n_tris;
+    info->instances = h.num_instances;
+    info->volumes = (int32_t)h.n_volumes;
+    info->bvh_nodes = (int32_t)h.n_nodes;
+    info->linear_ops = (int32_t)h.n_linear;
+    info->stack_need = cs.stack_need;
+    info->bytes_f32 = cs.blob32.size();
+    info->bytes_f64 = cs.blob64.size();
+  }
+  return s;
+}
+
 rt_status rt_render_tiles(rt_context* c, const rt_camera_desc* cam, const rt_render_params* prm, const rt_tile* tiles,
                           int32_t ntiles, void* out_rgb, int32_t out_is_device, void* stream) {
   if (!c) return set_err(nullptr, RT_ERR_INVALID_ARGUMENT, "null context");
@@ -887,8 +911,14 @@ rt_status rt_render_tiles(rt_context* c, const rt_camera_desc* cam, const rt_ren
   }
   RT_HIP(c, hipSetDevice(c->device));
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-  if (prm->precision == RT_PREC_F64) return render<double>(c, cam, prm, tiles, ntiles, out_rgb, out_is_device, st);
-  return render<float>(c, cam, prm, tiles, ntiles, out_rgb, out_is_device, st);
+  try {
+    if (prm->precision == RT_PREC_F64) return render<double>(c, cam, prm, tiles, ntiles, out_rgb, out_is_device, st);
+    return render<float>(c, cam, prm, tiles, ntiles, out_rgb, out_is_device, st);
+  } catch (const std::bad_alloc&) {
+    return set_err(c, RT_ERR_OUT_OF_MEMORY, "out of host memory");
+  } catch (const std::exception& e) {
+    return set_err(c, RT_ERR_INVALID_ARGUMENT, e.what());
+  }
 }
 
 rt_status rt_stats(rt_context* c, rt_counters* out) {

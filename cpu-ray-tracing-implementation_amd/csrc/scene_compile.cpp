@@ -19,6 +19,8 @@
 #include <cmath>
 #include <cstring>
 #include <limits>
+#include <new>
+#include <stdexcept>
 
 namespace rtd {
 namespace {
@@ -440,6 +442,10 @@ void Compiler::gather(int idx, const std::vector<Op>& chain, std::vector<Item>& 
       std::vector<Op> ops;
       const rt_object* w = o;
       while (w && is_wrapper(w->kind)) {
+        if ((int)(chain.size() + ops.size()) >= kMaxChain) {
+          fail("more than " + std::to_string(kMaxChain) + " nested translate/rotate wrappers (or a cycle)");
+          return;
+        }
         ops.push_back(op_of(*w));
         w = obj(w->child);
       }
@@ -479,6 +485,10 @@ void Compiler::gather(int idx, const std::vector<Op>& chain, std::vector<Item>& 
       std::vector<Op> ops;
       const rt_object* w = obj(o->child);
       while (w && is_wrapper(w->kind)) {
+        if ((int)(chain.size() + ops.size()) >= kMaxChain) {
+          fail("more than " + std::to_string(kMaxChain) + " nested translate/rotate wrappers (or a cycle)");
+          return;
+        }
         ops.push_back(op_of(*w));
         w = obj(w->child);
       }
@@ -771,8 +781,16 @@ rt_status compile_scene(const rt_scene_desc* desc, CompiledScene* out, std::stri
     *err = "world object index out of range";
     return RT_ERR_INVALID_ARGUMENT;
   }
-  Compiler c(desc);
-  if (!c.run(out, err)) return RT_ERR_UNSUPPORTED;
+  try {
+    Compiler c(desc);
+    if (!c.run(out, err)) return RT_ERR_UNSUPPORTED;
+  } catch (const std::bad_alloc&) {
+    *err = "out of host memory while compiling the scene";
+    return RT_ERR_OUT_OF_MEMORY;
+  } catch (const std::exception& e) {
+    *err = std::string("scene compilation failed: ") + e.what();
+    return RT_ERR_INVALID_ARGUMENT;
+  }
   return RT_OK;
 }
 

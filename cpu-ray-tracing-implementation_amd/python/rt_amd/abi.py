@@ -72,6 +72,12 @@ class rt_counters(ctypes.Structure):
                 ("last_render_ms", c_double), ("step_ms", c_double), ("aux_ms", c_double)]
 
 
+class rt_scene_info(ctypes.Structure):
+    _fields_ = [("quads", c_int32), ("spheres", c_int32), ("triangles", c_int32), ("instances", c_int32),
+                ("volumes", c_int32), ("bvh_nodes", c_int32), ("linear_ops", c_int32), ("stack_need", c_int32),
+                ("bytes_f32", c_uint64), ("bytes_f64", c_uint64)]
+
+
 # every symbol include/rt_hip.h declares, with its ctypes signature
 SIGNATURES = {
     "rt_abi_version": (c_int32, []),
@@ -79,6 +85,8 @@ SIGNATURES = {
     "rt_context_destroy": (None, [ctypes.c_void_p]),
     "rt_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
     "rt_scene_upload": (c_int32, [ctypes.c_void_p, ctypes.POINTER(rt_scene_desc)]),
+    "rt_scene_check": (c_int32, [ctypes.POINTER(rt_scene_desc), ctypes.POINTER(rt_scene_info), ctypes.c_char_p,
+                                 c_int32]),
     "rt_render_tiles": (c_int32, [ctypes.c_void_p, ctypes.POINTER(rt_camera_desc), ctypes.POINTER(rt_render_params),
                                   ctypes.POINTER(rt_tile), c_int32, ctypes.c_void_p, c_int32, ctypes.c_void_p]),
     "rt_stats": (c_int32, [ctypes.c_void_p, ctypes.POINTER(rt_counters)]),
@@ -108,6 +116,14 @@ def load():
             fn.argtypes = args
         _lib = lib
     return _lib
+
+
+def scene_check(desc):
+    """Compile a descriptor on the host (no GPU). Returns (status, rt_scene_info, message)."""
+    info = rt_scene_info()
+    err = ctypes.create_string_buffer(512)
+    st = load().rt_scene_check(ctypes.byref(desc), ctypes.byref(info), err, 512)
+    return st, info, err.value.decode()
 
 
 class RTError(RuntimeError):

@@ -1,0 +1,56 @@
+"""The C++ plugin surface (../../rt/*.h) as built into librt_scenes.so: the
+reference's main.cc config scenes assembled with camera / hittable / material
+objects, flattened exactly as camera::render flattens them."""
+import ctypes
+import os
+
+from . import abi
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        path = os.path.join(abi.BUILD_DIR, "librt_scenes.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} is missing: run `make`")
+        L = ctypes.CDLL(path)
+        P = ctypes.POINTER
+        L.rtsc_build.restype = ctypes.c_void_p
+        L.rtsc_build.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_double, P(abi.rt_scene_desc),
+                                 P(abi.rt_camera_desc), P(ctypes.c_int), P(ctypes.c_int), ctypes.c_char_p, ctypes.c_int]
+        L.rtsc_free.argtypes = [ctypes.c_void_p]
+        L.rtsc_render_ppm.restype = ctypes.c_int
+        L.rtsc_render_ppm.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_uint64, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+class ConfigScene:
+    """desc / cam / spp / max_depth of a main.cc scene built by the C++ plugin surface."""
+
+    def __init__(self, name, width=0, aspect=0.0):
+        L = load()
+        self.desc, self.cam = abi.rt_scene_desc(), abi.rt_camera_desc()
+        spp, depth = ctypes.c_int(), ctypes.c_int()
+        err = ctypes.create_string_buffer(256)
+        self._h = L.rtsc_build(name.encode(), width, aspect, ctypes.byref(self.desc), ctypes.byref(self.cam),
+                               ctypes.byref(spp), ctypes.byref(depth), err, 256)
+        if not self._h:
+            raise RuntimeError(f"rtsc_build({name}): {err.value.decode()}")
+        self.spp, self.max_depth = spp.value, depth.value
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.rtsc_free(self._h)
+            self._h = None
+
+
+def render_ppm(name, path, width=0, aspect=0.0, spp=0, max_depth=0, seed=1, precision=abi.RT_PREC_F32):
+    """camera::render(of, world, light) of a config scene into a PPM file (the whole drop-in path)."""
+    err = ctypes.create_string_buffer(512)
+    rc = load().rtsc_render_ppm(name.encode(), width, aspect, spp, max_depth, seed, precision, path.encode(), err, 512)
+    if rc != 0:
+        raise RuntimeError(f"camera::render failed: {err.value.decode()}")

@@ -1,0 +1,28 @@
+// hittable_list.h (reference: src/hittable_list.h:7-37): an ordered list; the
+// closest hit wins and, on equal t, the later object (kept on the device).
+#pragma once
+#include <memory>
+#include <vector>
+
+#include "hittable.h"
+
+class hittable_list : public hittable {
+ public:
+  std::vector<std::shared_ptr<hittable>> objects;
+  hittable_list() = default;
+  hittable_list(std::shared_ptr<hittable> object) { push_back(std::move(object)); }
+  void clear() { objects.clear(); }
+  void push_back(std::shared_ptr<hittable> object) { objects.push_back(std::move(object)); }
+  int flatten(scene_builder& sb) const override { return flatten_as(sb, RT_OBJ_LIST); }
+
+ protected:
+  int flatten_as(scene_builder& sb, int32_t kind) const {
+    std::vector<int> kids;
+    kids.reserve(objects.size());
+    for (const auto& o : objects) kids.push_back(sb.add(*o));
+    rt_object o = scene_builder::blank(kind);
+    o.first_child = sb.emit_children(kids);
+    o.child_count = (int32_t)kids.size();
+    return sb.emit_object(o);
+  }
+};

@@ -1,0 +1,85 @@
+// scene_builder.h -- serialises the plugin-surface objects (hittables,
+// materials, textures) into the POD rt_scene_desc of include/rt_hip.h.
+// Shared objects (the same shared_ptr used twice, e.g. the light quad that is
+// also in the world) map to one descriptor entry.
+#pragma once
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/rt_hip.h"
+#include "vec3.h"
+
+class hittable;
+class material;
+class texture;
+
+class unsupported_object : public std::runtime_error {
+ public:
+  using std::runtime_error::runtime_error;
+};
+
+class scene_builder {
+ public:
+  int add(const hittable& h);  // defined in hittable.h
+  int add_material(const material& m);
+  int add_texture(const texture& t);
+
+  // low-level emitters used by the classes' flatten()
+  int emit_object(const rt_object& o) {
+    objects_.push_back(o);
+    return (int)objects_.size() - 1;
+  }
+  rt_object& object(int i) { return objects_[(size_t)i]; }
+  int emit_children(const std::vector<int>& kids) {
+    int first = (int)children_.size();
+    children_.insert(children_.end(), kids.begin(), kids.end());
+    return first;
+  }
+  int emit_material(const rt_material& m) {
+    materials_.push_back(m);
+    return (int)materials_.size() - 1;
+  }
+  int emit_texture(const rt_texture& t) {
+    textures_.push_back(t);
+    return (int)textures_.size() - 1;
+  }
+
+  rt_scene_desc desc(int world, int light, int background) const {
+    rt_scene_desc d{};
+    d.objects = objects_.data();
+    d.num_objects = (int32_t)objects_.size();
+    d.children = children_.data();
+    d.num_children = (int32_t)children_.size();
+    d.materials = materials_.data();
+    d.num_materials = (int32_t)materials_.size();
+    d.textures = textures_.data();
+    d.num_textures = (int32_t)textures_.size();
+    d.world = world;
+    d.light = light;
+    d.background = background;
+    return d;
+  }
+
+  static void put3(double* dst, const vec3& v) {
+    dst[0] = v.x();
+    dst[1] = v.y();
+    dst[2] = v.z();
+  }
+  static rt_object blank(int32_t kind) {
+    rt_object o{};
+    o.kind = kind;
+    o.material = -1;
+    o.child = -1;
+    return o;
+  }
+
+ private:
+  std::vector<rt_object> objects_;
+  std::vector<int32_t> children_;
+  std::vector<rt_material> materials_;
+  std::vector<rt_texture> textures_;
+  std::unordered_map<const void*, int> seen_obj_, seen_mat_, seen_tex_;
+};

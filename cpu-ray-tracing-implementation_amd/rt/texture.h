@@ -1,0 +1,72 @@
+// texture.h -- textures of the plugin surface (reference: src/texture.h:6-63).
+// solid_color and checker_texture run on the device; a texture subclass the
+// device does not know makes camera::render fail with unsupported_object.
+#pragma once
+#include <memory>
+
+#include "color.h"
+#include "ray.h"
+#include "scene_builder.h"
+
+class texture {
+ public:
+  virtual ~texture() = default;
+  virtual color sample(double u, double v, point3 p) = 0;
+  // serialise into the descriptor; returns the texture index
+  virtual int flatten(scene_builder&) const { throw unsupported_object("texture type not supported on the device"); }
+};
+
+inline int scene_builder::add_texture(const texture& t) {
+  auto it = seen_tex_.find(&t);
+  if (it != seen_tex_.end()) return it->second;
+  int idx = t.flatten(*this);
+  seen_tex_[&t] = idx;
+  return idx;
+}
+
+class solid_color : public texture {
+ public:
+  solid_color(color c) : color_(c) {}
+  color sample(double, double, point3) override { return color_; }
+  int flatten(scene_builder& sb) const override {
+    rt_texture t{};
+    t.kind = RT_TEX_SOLID;
+    scene_builder::put3(t.color, color_);
+    return sb.emit_texture(t);
+  }
+  static std::shared_ptr<solid_color> black, white, red, green, blue, yellow, cyan, magenta;
+
+ private:
+  color color_;
+};
+inline std::shared_ptr<solid_color> solid_color::black = std::make_shared<solid_color>(color(0, 0, 0));
+inline std::shared_ptr<solid_color> solid_color::white = std::make_shared<solid_color>(color(1, 1, 1));
+inline std::shared_ptr<solid_color> solid_color::red = std::make_shared<solid_color>(color(1, 0, 0));
+inline std::shared_ptr<solid_color> solid_color::green = std::make_shared<solid_color>(color(0, 1, 0));
+inline std::shared_ptr<solid_color> solid_color::blue = std::make_shared<solid_color>(color(0, 0, 1));
+inline std::shared_ptr<solid_color> solid_color::yellow = std::make_shared<solid_color>(color(1, 1, 0));
+inline std::shared_ptr<solid_color> solid_color::cyan = std::make_shared<solid_color>(color(0, 1, 1));
+inline std::shared_ptr<solid_color> solid_color::magenta = std::make_shared<solid_color>(color(1, 0, 1));
+
+// 3D checker over floor(p / scale) (texture.h:39-63)
+class checker_texture : public texture {
+ public:
+  checker_texture(color odd, color even, double scale) : odd_(odd), even_(even), scale_(scale) {}
+  color sample(double, double, point3 p) override {
+    point3 q = p / scale_;
+    int total = int(std::floor(q.x())) + int(std::floor(q.y())) + int(std::floor(q.z()));
+    return total % 2 == 0 ? even_ : odd_;
+  }
+  int flatten(scene_builder& sb) const override {
+    rt_texture t{};
+    t.kind = RT_TEX_CHECKER;
+    scene_builder::put3(t.odd, odd_);
+    scene_builder::put3(t.even, even_);
+    t.scale = scale_;
+    return sb.emit_texture(t);
+  }
+
+ private:
+  color odd_, even_;
+  double scale_;
+};

@@ -1,0 +1,196 @@
+// config_scenes.cpp -- main.cc's config scenes on the plugin surface, plus a
+// small C ABI (rtsc_*) that tests and bench.py use to obtain the exact
+// descriptor camera::render would hand to librt_hip.
+#include "config_scenes.h"
+
+#include <cstring>
+#include <fstream>
+#include <vector>
+
+namespace {
+
+int W(int width, int dflt) { return width > 0 ? width : dflt; }
+double A(double aspect, double dflt) { return aspect > 0 ? aspect : dflt; }
+
+void cornell_box(int width, double aspect, config_scene* s) {  // main.cc:198-225
+  hittable_list world;
+  auto red = std::make_shared<lambertian>(std::make_shared<solid_color>(color{.65, .05, .05}));
+  auto white = std::make_shared<lambertian>(std::make_shared<solid_color>(color{0.73, 0.73, 0.73}));
+  auto green = std::make_shared<lambertian>(std::make_shared<solid_color>(color{.12, .45, .15}));
+  auto light = std::make_shared<diffuse_light>(std::make_shared<solid_color>(color{15, 15, 15}));
+  world.push_back(std::make_shared<quad>(point3(555, 0, 0), vec3(0, 555, 0), vec3(0, 0, 555), green));
+  world.push_back(std::make_shared<quad>(point3(0, 0, 0), vec3(0, 555, 0), vec3(0, 0, 555), red));
+  world.push_back(std::make_shared<quad>(point3(0, 0, 0), vec3(555, 0, 0), vec3(0, 0, 555), white));
+  world.push_back(std::make_shared<quad>(point3(555, 555, 555), vec3(-555, 0, 0), vec3(0, 0, -555), white));
+  world.push_back(std::make_shared<quad>(point3(0, 0, 555), vec3(555, 0, 0), vec3(0, 555, 0), white));
+  world.push_back(std::make_shared<translate>(vec3(100, 0, 200), box(point3(0), point3(165, 330, 165), white)));
+  world.push_back(std::make_shared<translate>(vec3(50, 0, 100), box(point3(0), point3(165, 165, 165), white)));
+  auto quad_light = std::make_shared<quad>(point3(343, 554, 332), vec3(-130, 0, 0), vec3(0, 0, -105), light);
+  world.push_back(quad_light);
+  s->world = std::make_shared<bvh_node>(world);
+  s->light = quad_light;
+  s->cam.initialize_perspective(W(width, 600), A(aspect, 1.0), point3(278, 278, -800), point3(278, 278, 0), 1,
+                                40.0, 40, 4);
+  s->cam.background_ = solid_color::black;
+}
+
+void cornell_box_with_volume(int width, double aspect, config_scene* s) {  // main.cc:227-253
+  auto world = std::make_shared<hittable_list>();
+  auto red = std::make_shared<lambertian>(color(.65, .05, .05));
+  auto white = std::make_shared<lambertian>(color(.73, .73, .73));
+  auto green = std::make_shared<lambertian>(color(.12, .45, .15));
+  auto light = std::make_shared<diffuse_light>(color(7, 7, 7));
+  world->push_back(std::make_shared<quad>(point3(555, 0, 0), vec3(0, 555, 0), vec3(0, 0, 555), green));
+  world->push_back(std::make_shared<quad>(point3(0, 0, 0), vec3(0, 555, 0), vec3(0, 0, 555), red));
+  world->push_back(std::make_shared<quad>(point3(0, 555, 0), vec3(555, 0, 0), vec3(0, 0, 555), white));
+  world->push_back(std::make_shared<quad>(point3(0, 0, 0), vec3(555, 0, 0), vec3(0, 0, 555), white));
+  world->push_back(std::make_shared<quad>(point3(0, 0, 555), vec3(555, 0, 0), vec3(0, 555, 0), white));
+  auto box1 = std::make_shared<translate>(
+      vec3(265, 0, 285), std::make_shared<rotate_y>(box(point3(0), point3(150, 280, 150), white), 45));
+  auto box2 = std::make_shared<translate>(
+      vec3(130, 0, 65), std::make_shared<rotate_y>(box(point3(0), point3(140, 140, 140), white), -15));
+  world->push_back(std::make_shared<volumne>(box1, 0.02, std::make_shared<solid_color>(color(0))));
+  world->push_back(std::make_shared<volumne>(box2, 0.02, std::make_shared<solid_color>(color(1))));
+  auto quad_light = std::make_shared<quad>(point3(113, 554, 127), vec3(330, 0, 0), vec3(0, 0, 305), light);
+  world->push_back(quad_light);
+  s->world = world;
+  s->light = quad_light;
+  s->cam.initialize_perspective(W(width, 600), A(aspect, 1.0), point3(278, 278, -800), point3(278, 278, 0), 1, 40,
+                                100, 5);
+  s->cam.background_ = solid_color::black;
+}
+
+// main.cc:105-153. `moving` keeps the reference's moving spheres (whose normals use
+// center_ = (0,0,0), sphere.h:69); the static variant places each sphere at center1
+// and still draws center2, so the random stream and the sphere list are unchanged.
+void random_motion_ball(int width, double aspect, bool moving, config_scene* s) {
+  std::srand(1);  // the reference never seeds: glibc's default state is srand(1)
+  hittable_list world;
+  auto ground = std::make_shared<lambertian>(
+      std::make_shared<checker_texture>(color{1.0, 1.0, 1.0}, color{0.6, 0.6, 0.2}, 1.0));
+  world.push_back(std::make_shared<sphere>(point3(0, -1000, 0), 1000, ground));
+  for (int a = -11; a < 11; a++) {
+    for (int b = -11; b < 11; b++) {
+      double choose_mat = random_double();
+      double rz = random_double();  // GCC evaluates center1's arguments right to left
+      double rx = random_double();
+      point3 center1(a + 0.7 * rx, 0.2, b + 0.7 * rz);
+      point3 center2 = center1 + vec3(0, random_double(0, .15), 0);
+      if ((center1 - point3(4, 0.2, 0)).length() <= 0.9 || choose_mat < 0.3) continue;
+      std::shared_ptr<material> m;
+      if (choose_mat < 0.8) {
+        vec3 rhs = random_vec();  // random_vec() * random_vec(): right operand first
+        vec3 lhs = random_vec();
+        m = std::make_shared<lambertian>(std::make_shared<solid_color>(lhs * rhs));
+      } else if (choose_mat < 0.95) {
+        m = std::make_shared<metal>(std::make_shared<solid_color>(random_vec(0.5, 1)), 0.0);
+      } else {
+        m = std::make_shared<dielectric>(std::make_shared<solid_color>(color(1)), 1.5);
+      }
+      if (moving)
+        world.push_back(std::make_shared<sphere>(center1, center2, 0.2, m));
+      else
+        world.push_back(std::make_shared<sphere>(center1, 0.2, m));
+    }
+  }
+  auto glass = std::make_shared<dielectric>(std::make_shared<solid_color>(color(1)), 1.5);
+  auto matte = std::make_shared<lambertian>(std::make_shared<solid_color>(color(0.4, 0.2, 0.1)));
+  world.push_back(std::make_shared<sphere>(point3(0, 1, 0), 1.0, glass));
+  world.push_back(std::make_shared<sphere>(point3(-4, 1, 0), 1.0, matte));
+  world.push_back(std::make_shared<sphere>(point3(4, 1, 0), 1.0, glass));
+  s->world = std::make_shared<bvh_node>(world);
+  s->cam.initialize_perspective(W(width, 1280), A(aspect, 16.0 / 9.0), point3(13, 2, 3), point3(0, 0, 0), 1, 20,
+                                20, 50);
+  s->cam.background_ = std::make_shared<solid_color>(color(0.7, 0.8, 1.0));
+}
+
+void three_material_ball(int width, double aspect, config_scene* s) {  // main.cc:67-84
+  auto world = std::make_shared<hittable_list>();
+  auto ground = std::make_shared<lambertian>(
+      std::make_shared<checker_texture>(color{1.0, 1.0, 1.0}, color{0.6, 0.6, 0.2}, 1.0));
+  auto glass = std::make_shared<dielectric>(std::make_shared<solid_color>(color{1.0, 1.0, 1.0}), 1.5);
+  auto matte = std::make_shared<lambertian>(std::make_shared<solid_color>(color(0.4, 0.2, 0.1)));
+  auto metal_mat = std::make_shared<metal>(std::make_shared<solid_color>(color(0.7, 0.6, 0.5)), 0.0);
+  world->push_back(std::make_shared<sphere>(point3(0, -1000, 0), 1000, ground));
+  world->push_back(std::make_shared<sphere>(point3(0, 1, 0), 1.0, glass));
+  world->push_back(std::make_shared<sphere>(point3(-4, 1, 0), 1.0, matte));
+  world->push_back(std::make_shared<sphere>(point3(4, 1, 0), 1.0, metal_mat));
+  s->world = world;
+  s->cam.initialize_perspective(W(width, 1280), A(aspect, 16.0 / 9.0), point3(13, 2, 3), vec3(0, 0, 0), 1, 20.0,
+                                100, 5);
+  s->cam.background_ = std::make_shared<solid_color>(color(0.7, 0.8, 1.0));
+}
+
+}  // namespace
+
+bool build_config_scene(const std::string& name, int width, double aspect, config_scene* out) {
+  if (name == "cornell_box")
+    cornell_box(width, aspect, out);
+  else if (name == "cornell_box_with_volume")
+    cornell_box_with_volume(width, aspect, out);
+  else if (name == "rtow" || name == "rtow_motion")
+    random_motion_ball(width, aspect, name == "rtow_motion", out);
+  else if (name == "three_material_ball")
+    three_material_ball(width, aspect, out);
+  else
+    return false;
+  return true;
+}
+
+// ---------------------------------------------------------------- C ABI for tests / bench
+struct rtsc_handle {
+  config_scene scene;
+  scene_builder sb;
+  rt_scene_desc desc{};
+};
+
+extern "C" {
+
+// Builds a config scene and returns its descriptor and camera (owned by the handle).
+void* rtsc_build(const char* name, int width, double aspect, rt_scene_desc* desc, rt_camera_desc* cam, int* spp,
+                 int* max_depth, char* err, int errlen) {
+  auto h = std::make_unique<rtsc_handle>();
+  auto fail = [&](const std::string& m) -> void* {
+    if (err && errlen > 0) std::snprintf(err, (size_t)errlen, "%s", m.c_str());
+    return nullptr;
+  };
+  if (!name || !build_config_scene(name, width, aspect, &h->scene)) return fail("unknown scene");
+  try {
+    int w = h->sb.add(*h->scene.world);
+    int l = h->scene.light ? h->sb.add(*h->scene.light) : -1;
+    int bg = h->scene.cam.background_ ? h->sb.add_texture(*h->scene.cam.background_) : -1;
+    h->desc = h->sb.desc(w, l, bg);
+  } catch (const unsupported_object& e) {
+    return fail(e.what());
+  }
+  if (desc) *desc = h->desc;
+  if (cam) *cam = h->scene.cam.describe();
+  if (spp) *spp = h->scene.cam.samples_per_pixel_;
+  if (max_depth) *max_depth = h->scene.cam.max_recur_depth_;
+  return h.release();
+}
+
+void rtsc_free(void* h) { delete static_cast<rtsc_handle*>(h); }
+
+// The full drop-in path: build the scene, camera::render(of, world, light) to a PPM file.
+int rtsc_render_ppm(const char* name, int width, double aspect, int spp, int max_depth, uint64_t seed, int precision,
+                    const char* path, char* err, int errlen) {
+  config_scene s;
+  if (!name || !build_config_scene(name, width, aspect, &s)) {
+    if (err && errlen > 0) std::snprintf(err, (size_t)errlen, "unknown scene");
+    return 1;
+  }
+  if (spp > 0) s.cam.samples_per_pixel_ = spp;
+  if (max_depth > 0) s.cam.max_recur_depth_ = max_depth;
+  s.cam.seed_ = seed;
+  s.cam.precision_ = precision == RT_PREC_F64 ? RT_PREC_F64 : RT_PREC_F32;
+  std::ofstream of(path);
+  s.cam.render(of, *s.world, s.light);
+  if (!s.cam.last_error_.empty()) {
+    if (err && errlen > 0) std::snprintf(err, (size_t)errlen, "%s", s.cam.last_error_.c_str());
+    return 2;
+  }
+  return 0;
+}
+
+}  // extern "C"

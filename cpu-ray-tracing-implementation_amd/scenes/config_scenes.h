@@ -1,0 +1,23 @@
+// config_scenes.h -- the reference's main.cc scenes that BASELINE.json's configs
+// use, written against the plugin surface exactly as a main.cc caller would.
+#pragma once
+#include <memory>
+#include <string>
+
+#include "../rt/bvh_node.h"
+#include "../rt/camera.h"
+#include "../rt/hittable_list.h"
+#include "../rt/quad.h"
+#include "../rt/sphere.h"
+#include "../rt/triangle.h"
+#include "../rt/volumne.h"
+
+struct config_scene {
+  std::shared_ptr<hittable> world;
+  std::shared_ptr<hittable> light;  // importance-sampled light or null
+  camera cam;
+};
+
+// name: cornell_box | cornell_box_with_volume | rtow | rtow_motion | three_material_ball.
+// width/aspect <= 0 keep the scene's own camera. Returns false for an unknown name.
+bool build_config_scene(const std::string& name, int width, double aspect, config_scene* out);

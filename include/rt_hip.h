@@ -193,6 +193,15 @@ typedef struct rt_counters {
   double aux_ms;  /* reserved */
 } rt_counters;
 
+/* What rt_scene_check / rt_scene_upload compiled a descriptor into. */
+typedef struct rt_scene_info {
+  int32_t quads, spheres, triangles, instances, volumes, bvh_nodes;
+  int32_t linear_ops; /* > 0: small scene traversed as a wave-uniform linear program */
+  int32_t stack_need; /* traversal stack entries a ray can need (BVH path) */
+  uint64_t bytes_f32; /* device scene size, fp32 / fp64 paths */
+  uint64_t bytes_f64;
+} rt_scene_info;
+
 typedef struct rt_context rt_context;
 
 /* Library / ABI version, for the binding to check. */
@@ -207,6 +216,10 @@ const char* rt_last_error(const rt_context* ctx);
 /* Compile the hittable DAG (BVH build, instance transforms, volumes) and upload
  * it. The library copies everything it needs; desc may be freed afterwards. */
 rt_status rt_scene_upload(rt_context* ctx, const rt_scene_desc* desc);
+
+/* Host-only: compile the descriptor exactly as rt_scene_upload would, without a
+ * device. Returns RT_OK, RT_ERR_INVALID_ARGUMENT or RT_ERR_UNSUPPORTED (message in err). */
+rt_status rt_scene_check(const rt_scene_desc* desc, rt_scene_info* info, char* err, int32_t errlen);
 
 /* Render `ntiles` rectangles of the image described by `cam`. */
 rt_status rt_render_tiles(rt_context* ctx, const rt_camera_desc* cam, const rt_render_params* params,

@@ -1,0 +1,118 @@
+"""The C ABI (include/rt_hip.h) without a GPU: every declared symbol is exported,
+the ctypes structs match the C compiler's layout, scene compilation and its
+errors, and clean failure when no device is present."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from rt_amd import abi, scenes
+from rt_amd.scene import SceneBuilder
+
+HDR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "rt_hip.h")
+STRUCTS = ["rt_object", "rt_material", "rt_texture", "rt_scene_desc", "rt_camera_desc", "rt_render_params",
+           "rt_tile", "rt_counters", "rt_scene_info"]
+
+
+def declared_functions():
+    text = open(HDR).read()
+    return sorted(set(re.findall(r"^\s*(?:rt_status|void|const char\*|int32_t|uint32_t)\s+(rt_\w+)\(", text, re.M)))
+
+
+def test_every_declared_symbol_is_exported():
+    lib = abi.load()
+    names = declared_functions()
+    assert len(names) >= 10
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(abi.SIGNATURES), set(names) ^ set(abi.SIGNATURES)
+    assert lib.rt_abi_version() == 1
+
+
+def test_struct_layout_matches_c(tmp_path):
+    prog = tmp_path / "layout.c"
+    prog.write_text('#include "%s"\n#include <stdio.h>\nint main(void){\n' % HDR +
+                    "".join(f'printf("{s} %zu\\n", sizeof({s}));\n' for s in STRUCTS) + "return 0;}\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-o", str(exe), str(prog)], check=True)
+    sizes = dict(line.split() for line in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split("\n")
+                 if line)
+    for s in STRUCTS:
+        assert ctypes.sizeof(getattr(abi, s)) == int(sizes[s]), s
+
+
+def test_context_create_without_device_fails_cleanly():
+    import torch
+    if torch.cuda.device_count() > 0:
+        pytest.skip("a GPU is present")
+    lib = abi.load()
+    h = ctypes.c_void_p()
+    assert lib.rt_context_create(0, ctypes.byref(h)) == abi.RT_ERR_NO_DEVICE
+    assert not h.value
+    assert b"device" in lib.rt_last_error(None)
+
+
+@pytest.mark.parametrize("name,quads,spheres,linear", [("cornell_box", 18, 0, True),
+                                                       ("cornell_box_with_volume", 18, 0, True),
+                                                       ("three_material_ball", 0, 4, True), ("rtow", 0, 339, False)])
+def test_scene_check_config_scenes(name, quads, spheres, linear):
+    desc, _, _, _ = scenes.SCENES[name](width=16)
+    st, info, msg = abi.scene_check(desc)
+    assert st == abi.RT_OK, msg
+    assert (info.quads, info.spheres) == (quads, spheres)
+    assert (info.linear_ops > 0) == linear
+    if not linear:
+        assert info.bvh_nodes > 0 and 1 <= info.stack_need <= 32
+
+
+def test_scene_check_volume_list_keeps_reference_order():
+    desc, _, _, _ = scenes.cornell_box_with_volume(width=16)
+    st, info, _ = abi.scene_check(desc)
+    assert st == abi.RT_OK and info.volumes == 2 and info.instances == 2 and info.bvh_nodes == 0
+
+
+def test_unsupported_material_is_rejected():
+    s = SceneBuilder()
+    m = s._mat(abi.RT_MAT_GLOSS, s.solid((1, 1, 1)))
+    st, _, msg = abi.scene_check(s.desc(s.sphere((0, 0, 0), 1, m)))
+    assert st == abi.RT_ERR_UNSUPPORTED and "material kind" in msg
+
+
+def test_bad_descriptors_are_rejected():
+    s = SceneBuilder()
+    m = s.lambertian(s.solid((1, 1, 1)))
+    q = s.quad((0, 0, 0), (1, 0, 0), (0, 1, 0), m)
+    st, _, msg = abi.scene_check(s.desc(q + 5))
+    assert st == abi.RT_ERR_INVALID_ARGUMENT
+    # a primitive without a material
+    s2 = SceneBuilder()
+    st, _, msg = abi.scene_check(s2.desc(s2.sphere((0, 0, 0), 1, -1)))
+    assert st == abi.RT_ERR_UNSUPPORTED and "material" in msg
+    # a cycle in the object graph
+    s3 = SceneBuilder()
+    t = s3.translate(0, (1, 0, 0))  # child 0 = itself
+    st, _, msg = abi.scene_check(s3.desc(t))
+    assert st != abi.RT_OK
+    # a volume whose boundary mixes two different wrapper chains
+    s4 = SceneBuilder()
+    m4 = s4.lambertian(s4.solid((1, 1, 1)))
+    b = s4.hlist([s4.translate(s4.box((0, 0, 0), (1, 1, 1), m4), (1, 0, 0)),
+                  s4.translate(s4.box((0, 0, 0), (1, 1, 1), m4), (3, 0, 0))])
+    st, _, msg = abi.scene_check(s4.desc(s4.volume(b, 0.1, s4.solid((1, 1, 1)))))
+    assert st == abi.RT_ERR_UNSUPPORTED and "volume boundary" in msg
+
+
+def test_big_scene_gets_a_bvh_within_the_stack():
+    import random
+    rnd = random.Random(3)
+    s = SceneBuilder()
+    m = s.lambertian(s.solid((0.5, 0.5, 0.5)))
+    tris = []
+    for _ in range(20000):
+        c = [rnd.uniform(-50, 50) for _ in range(3)]
+        tris.append(s.triangle(c, [c[0] + rnd.random(), c[1], c[2]], [c[0], c[1] + rnd.random(), c[2]], m))
+    st, info, msg = abi.scene_check(s.desc(s.bvh(tris)))
+    assert st == abi.RT_OK, msg
+    assert info.triangles == 20000 and info.linear_ops == 0 and info.stack_need <= 32
