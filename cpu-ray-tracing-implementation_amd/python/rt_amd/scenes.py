@@ -36,6 +36,40 @@ def cornell_box(width=600, aspect=1.0):  # main.cc:198-225
     return s.desc(world, light=lq, background=s.solid((0, 0, 0))), cam, 40, 4
 
 
+def cornell_triangles(width=600, aspect=1.0):
+    """cornell_box with every wall/box quad split into triangles (q, q+u, q+v), (q+u+v, q+v, q+u):
+    exercises triangle.h on the main.cc Cornell scene (the oracle builds the same)."""
+    s = SceneBuilder()
+    red = s.lambertian(s.solid((.65, .05, .05)))
+    white = s.lambertian(s.solid((0.73, 0.73, 0.73)))
+    green = s.lambertian(s.solid((.12, .45, .15)))
+    light = s.diffuse_light(s.solid((15, 15, 15)))
+    add = lambda v, w: tuple(a + b for a, b in zip(v, w))
+
+    def tris(q, u, v, m):
+        return [s.triangle(q, add(q, u), add(q, v), m), s.triangle(add(add(q, u), v), add(q, v), add(q, u), m)]
+
+    def box(a, b, m):
+        dx, dy, dz = (b[0] - a[0], 0, 0), (0, b[1] - a[1], 0), (0, 0, b[2] - a[2])
+        neg = lambda v: tuple(-x for x in v)
+        out = []
+        for q, u, v in [((a[0], a[1], b[2]), dy, dx), ((b[0], a[1], b[2]), dy, neg(dz)), ((b[0], a[1], a[2]), dy, neg(dx)),
+                        ((a[0], a[1], a[2]), dy, dz), ((a[0], b[1], b[2]), neg(dz), dx), ((a[0], a[1], a[2]), dz, dx)]:
+            out += tris(q, u, v, m)
+        return s.hlist(out)
+
+    w = (tris((555, 0, 0), (0, 555, 0), (0, 0, 555), green) + tris((0, 0, 0), (0, 555, 0), (0, 0, 555), red) +
+         tris((0, 0, 0), (555, 0, 0), (0, 0, 555), white) + tris((555, 555, 555), (-555, 0, 0), (0, 0, -555), white) +
+         tris((0, 0, 555), (555, 0, 0), (0, 555, 0), white))
+    w.append(s.translate(box((0, 0, 0), (165, 330, 165), white), (100, 0, 200)))
+    w.append(s.translate(box((0, 0, 0), (165, 165, 165), white), (50, 0, 100)))
+    lq = s.quad((343, 554, 332), (-130, 0, 0), (0, 0, -105), light)  # the light stays a quad (importance-sampled)
+    w.append(lq)
+    world = s.bvh(w)
+    cam = perspective(width, aspect, (278, 278, -800), (278, 278, 0), 1, 40.0)
+    return s.desc(world, light=lq, background=s.solid((0, 0, 0))), cam, 40, 4
+
+
 def cornell_box_with_volume(width=600, aspect=1.0):  # main.cc:227-253
     s = SceneBuilder()
     red = s.lambertian(s.solid((.65, .05, .05)))
@@ -100,6 +134,6 @@ def three_material_ball(width=1280, aspect=16.0 / 9.0):  # main.cc:67-84
     return s.desc(world, background=s.solid((0.7, 0.8, 1.0))), cam, 100, 5
 
 
-SCENES = {"cornell_box": cornell_box, "cornell_box_with_volume": cornell_box_with_volume,
+SCENES = {"cornell_box": cornell_box, "cornell_triangles": cornell_triangles, "cornell_box_with_volume": cornell_box_with_volume,
           "rtow": rtow, "rtow_motion": lambda **kw: rtow(moving=True, **kw),
           "three_material_ball": three_material_ball}

@@ -164,7 +164,8 @@ typedef struct rt_render_params {
   uint64_t seed;            /* counter-RNG key; pixel (x, y) sample s is keyed by (seed, y*W+x, s) */
   int32_t precision;        /* rt_precision */
   int32_t first_sample;     /* render samples [first_sample, first_sample + spp) of each pixel */
-  int32_t samples_per_item; /* samples one work item accumulates (0 = auto). Does not change the image. */
+  int32_t samples_per_item; /* samples one work item accumulates (0 = auto: min(spp, 16)). The per-pixel sum
+                               is grouped by item, so this changes the image only by rounding. */
   int32_t pool_slots;       /* wavefront pool size (0 = auto). Does not change the image. */
   int32_t segments_per_launch; /* segments each path slot advances per kernel launch (0 = auto).
                                   Does not change the image. */
