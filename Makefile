@@ -19,6 +19,18 @@ $(BUILD)/librt_hip.so: $(LIB_SRCS) $(LIB_HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(LIB_SRCS)
 
+# development build with correctly rounded fp32 math (scripts/dev_divergence.py --lib)
+precise: $(BUILD)/librt_hip_precise.so
+$(BUILD)/librt_hip_precise.so: $(LIB_SRCS) $(LIB_HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DRT_PRECISE_F32 -shared -o $@ $(LIB_SRCS)
+
+# development build printing every traced segment (scripts/dev_sample_trace.py)
+trace: $(BUILD)/librt_hip_trace.so
+$(BUILD)/librt_hip_trace.so: $(LIB_SRCS) $(LIB_HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DRT_DEBUG_TRACE -shared -o $@ $(LIB_SRCS)
+
 # the reference's config scenes written against the drop-in plugin surface (+ rtsc_* C ABI for tests)
 $(BUILD)/librt_scenes.so: $(PKG)/scenes/config_scenes.cpp $(PKG)/scenes/config_scenes.h $(RT_HDRS) $(BUILD)/librt_hip.so
 	$(CXX) $(CXXFLAGS) -shared -o $@ $(PKG)/scenes/config_scenes.cpp -L$(BUILD) -lrt_hip -Wl,-rpath,'$$ORIGIN'
@@ -34,4 +46,4 @@ clean:
 	rm -rf $(BUILD)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean precise trace

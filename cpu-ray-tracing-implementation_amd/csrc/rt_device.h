@@ -11,6 +11,44 @@
 
 namespace rtd {
 
+// Math policy. fp64 (the parity path): IEEE division/sqrt and libm, as the reference.
+// fp32 (the production path): the hardware ops -- v_rcp_f32, v_sqrt_f32, v_rsq_f32,
+// v_log_f32, and v_sin_f32 / v_cos_f32, which take their argument in revolutions, so
+// sin(2*pi*u) for u in [0,1) needs no range reduction.
+// RT_PRECISE_F32 (a development build, see scripts/dev_divergence.py) swaps the fp32 ops
+// for the correctly rounded ones to measure what the hardware ops cost in path divergence.
+#ifndef RT_PRECISE_F32
+__device__ __forceinline__ float fdiv(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+__device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float flog(float x) { return __builtin_amdgcn_logf(x) * 0.693147180559945309f; }
+__device__ __forceinline__ float frsq(float x) { return __builtin_amdgcn_rsqf(x); }
+__device__ __forceinline__ void sincos2pi(float u, float& s, float& c) {
+  s = __builtin_amdgcn_sinf(u);
+  c = __builtin_amdgcn_cosf(u);
+}
+#else
+__device__ __forceinline__ float fdiv(float a, float b) { return a / b; }
+__device__ __forceinline__ float fsqrt(float x) { return sqrtf(x); }
+__device__ __forceinline__ float flog(float x) { return logf(x); }
+__device__ __forceinline__ float frsq(float x) { return 1.0f / sqrtf(x); }
+__device__ __forceinline__ void sincos2pi(float u, float& s, float& c) {
+  float phi = 2 * 3.14159265358979f * u;
+  s = sinf(phi);
+  c = cosf(phi);
+}
+#endif
+__device__ __forceinline__ double fdiv(double a, double b) { return a / b; }
+__device__ __forceinline__ double fsqrt(double x) { return sqrt(x); }
+__device__ __forceinline__ double flog(double x) { return log(x); }
+// sin(2*pi*u), cos(2*pi*u); the fp64 form evaluates phi = 2*pi*u first like utility.h:36,64
+__device__ __forceinline__ void sincos2pi(double u, double& s, double& c) {
+  double phi = 2 * 3.1415926535897932385 * u;
+  s = sin(phi);
+  c = cos(phi);
+}
+__device__ __forceinline__ float pow5(float x) { return (x * x) * (x * x) * x; }
+__device__ __forceinline__ double pow5(double x) { return pow(x, 5.0); }
+
 // ------------------------------------------------------------------ vectors
 template <class R>
 struct V {
@@ -61,13 +99,9 @@ __device__ __forceinline__ V<R> cross(V<R> a, V<R> b) {  // vec3.h:79-82
   return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
 }
 template <class R>
-__device__ __forceinline__ R len(V<R> a) {
-  return sqrt(a.x * a.x + a.y * a.y + a.z * a.z);
-}
+__device__ __forceinline__ R len(V<R> a);
 template <class R>
-__device__ __forceinline__ V<R> unit(V<R> a) {  // vec3.h:77
-  return a / len(a);
-}
+__device__ __forceinline__ V<R> unit(V<R> a);
 template <class R>
 __device__ __forceinline__ V<R> reflect(V<R> v, V<R> n) {  // utility.h:70
   return v - (R(2) * dot(v, n)) * n;
@@ -76,13 +110,23 @@ template <class R>
 __device__ __forceinline__ V<R> refract(V<R> v, V<R> n, R eta) {  // utility.h:71-76
   R cos_theta = fmin(dot(-v, n), R(1));
   V<R> perp = eta * (v + cos_theta * n);
-  V<R> par = (-sqrt(fabs(R(1) - dot(perp, perp)))) * n;
+  V<R> par = (-fsqrt(fabs(R(1) - dot(perp, perp)))) * n;
   return perp + par;
 }
 
-// a / b: exact IEEE division for the fp64 parity path, v_rcp_f32-based for the fp32 path
-__device__ __forceinline__ float fdiv(float a, float b) { return __fdividef(a, b); }
-__device__ __forceinline__ double fdiv(double a, double b) { return a / b; }
+
+template <class R>
+__device__ __forceinline__ R len(V<R> a) {
+  return fsqrt(a.x * a.x + a.y * a.y + a.z * a.z);
+}
+template <>
+__device__ __forceinline__ V<float> unit(V<float> a) {  // vec3.h:77 (v / |v|), as v * rsqrt(v.v)
+  return a * frsq(a.x * a.x + a.y * a.y + a.z * a.z);
+}
+template <>
+__device__ __forceinline__ V<double> unit(V<double> a) {  // vec3.h:77
+  return a / len(a);
+}
 
 template <class R>
 struct Num;
@@ -116,8 +160,10 @@ __host__ __device__ __forceinline__ uint32_t key_pixel(uint64_t seed, uint32_t p
 __host__ __device__ __forceinline__ uint32_t key_sample(uint64_t seed, uint32_t sample) {
   return mix32(sample + mix32((uint32_t)(seed >> 32) + 0x7F4A7C15u));
 }
-__host__ __device__ __forceinline__ uint32_t draw_u32(uint32_t ka, uint32_t kb, uint32_t dim) {
-  return mix32(ka ^ mix32(kb + dim * 0x9E3779B9u));
+// the key of one camera sample; each draw is then a single mix (two 32-bit multiplies)
+__host__ __device__ __forceinline__ uint32_t key_path(uint32_t ka, uint32_t kb) { return mix32(ka ^ kb); }
+__host__ __device__ __forceinline__ uint32_t draw_u32(uint32_t ks, uint32_t dim) {
+  return mix32(ks + dim * 0x9E3779B9u);
 }
 template <class R>
 __device__ __forceinline__ R to_unit(uint32_t x) {  // exact 24-bit value in [0,1)
@@ -134,7 +180,7 @@ __device__ __forceinline__ uint32_t dim_scatter(uint32_t bounce, uint32_t j) {
 }
 
 struct Keys {
-  uint32_t ka, kb;
+  uint32_t ks;  // key_path of the camera sample
 };
 
 // ------------------------------------------------------------------ scene view
@@ -150,7 +196,7 @@ struct DevScene {
   const Material<R>* mats;
   const Texture<R>* texs;
   const Light<R>* light;
-  const uint32_t* linear;
+  const LinRec<R>* lin;  // linear program (n_linear > 0)
   uint32_t n_linear;
   uint32_t root;
   int32_t background;
@@ -241,19 +287,44 @@ __device__ __forceinline__ bool tri_t(const Tri<R>& tr, V<R> o, V<R> d, R tmin, 
 // sphere::hit (sphere.h:40-74). `far_only` is used for the sphere the ray
 // starts on: in exact arithmetic its near root is 0 (rejected by the 0.001
 // interval) and the ray re-enters only if it points inside.
+//
+// fp64 evaluates the reference's formula as written. In fp32 that formula loses
+// the hit: b^2 - 4ac cancels for a small sphere seen from afar (|o-c|^2 ~ 85 for
+// a unit sphere 9 away leaves t ~1e-5 off, which two mirror bounces turn into a
+// different path). fp32 therefore takes the discriminant from the ray's
+// perpendicular distance to the center, a (r^2 - |l|^2) with l = f - (f.d/a) d,
+// and the roots in the cancellation-free form q/a, c/q (Ray Tracing Gems I, ch. 7):
+// the same roots, accurate to fp32 rounding.
 template <class T>
 __device__ __forceinline__ bool sphere_roots(T ox, T oy, T oz, T dx, T dy, T dz, T cx, T cy, T cz, T r, T tmin,
                                              T tmax, bool far_only, T& t) {
   T fx = ox - cx, fy = oy - cy, fz = oz - cz;
   T a = dx * dx + dy * dy + dz * dz;
-  T b = T(2) * (dx * fx + dy * fy + dz * fz);
-  T c = (fx * fx + fy * fy + fz * fz) - r * r;
-  T disc = b * b - T(4) * a * c;
-  if (disc < T(0)) return false;
-  T sq = sqrt(disc);
-  T root = (-b - sq) / (T(2) * a);
+  T lo, hi;
+  if constexpr (sizeof(T) == 8) {
+    T b = T(2) * (dx * fx + dy * fy + dz * fz);
+    T c = (fx * fx + fy * fy + fz * fz) - r * r;
+    T disc = b * b - T(4) * a * c;
+    if (disc < T(0)) return false;
+    T sq = fsqrt(disc);
+    lo = (-b - sq) / (T(2) * a);
+    hi = (-b + sq) / (T(2) * a);
+  } else {
+    T ia = fdiv(T(1), a);
+    T bh = -(dx * fx + dy * fy + dz * fz);  // -b/2
+    T s = bh * ia;
+    T lx = fx + s * dx, ly = fy + s * dy, lz = fz + s * dz;
+    T disc = a * (r * r - (lx * lx + ly * ly + lz * lz));
+    if (disc < T(0)) return false;
+    T q = bh + copysignf(fsqrt(disc), bh);
+    T c = (fx * fx + fy * fy + fz * fz) - r * r;
+    T t0 = fdiv(c, q), t1 = q * ia;
+    lo = fminf(t0, t1);
+    hi = fmaxf(t0, t1);
+  }
+  T root = lo;
   if (far_only || !(tmin <= root && root <= tmax)) {
-    root = (-b + sq) / (T(2) * a);
+    root = hi;
     if (!(tmin <= root && root <= tmax)) return false;
   }
   t = root;
@@ -268,22 +339,73 @@ __device__ __forceinline__ V<R> sphere_center(const Sphere<R>& s, R time) {  // 
 }
 
 template <class R>
-__device__ __forceinline__ bool sphere_t(const Sphere<R>& s, V<R> o, V<R> d, R time, R tmin, R tmax, bool self, R& t) {
-  V<R> c = sphere_center(s, time);
+__device__ __forceinline__ bool sphere_test(V<R> c1, V<R> dc, R r, bool moving, V<R> o, V<R> d, R time, R tmin,
+                                            R tmax, bool self, R& t) {
+  V<R> c = moving ? c1 + time * dc : c1;  // sphere.h:83
   bool far_only = false;
   if (self) {
     if (dot(d, o - c) >= R(0)) return false;  // leaving the sphere it starts on
     far_only = true;
   }
-  if (sizeof(R) == 4 && s.r > R(16)) {
+  if (sizeof(R) == 4 && r > R(16)) {
     // big spheres (the RTOW ground, r = 1000): |o-c|^2 - r^2 cancels catastrophically in fp32
     double td;
-    if (!sphere_roots<double>(o.x, o.y, o.z, d.x, d.y, d.z, c.x, c.y, c.z, s.r, tmin, tmax, far_only, td))
+    if (!sphere_roots<double>(o.x, o.y, o.z, d.x, d.y, d.z, c.x, c.y, c.z, r, tmin, tmax, far_only, td))
       return false;
     t = (R)td;
     return true;
   }
-  return sphere_roots<R>(o.x, o.y, o.z, d.x, d.y, d.z, c.x, c.y, c.z, s.r, tmin, tmax, far_only, t);
+  return sphere_roots<R>(o.x, o.y, o.z, d.x, d.y, d.z, c.x, c.y, c.z, r, tmin, tmax, far_only, t);
+}
+template <class R>
+__device__ __forceinline__ bool sphere_t(const Sphere<R>& s, V<R> o, V<R> d, R time, R tmin, R tmax, bool self, R& t) {
+  return sphere_test(ld3(s.c1), ld3(s.dc), s.r, s.moving != 0, o, d, time, tmin, tmax, self, t);
+}
+
+// Axis-aligned quad (rt_scene.h LinRec): n = +-e_A exactly, so quad.h:32-33 reduce to
+// t = (q_A - o_A) / d_A bit for bit; alpha = (p_U - q_U) / u_U, beta = (p_V - q_V) / v_V.
+template <int K, class R>
+__device__ __forceinline__ R comp(V<R> v) {
+  return K == 0 ? v.x : (K == 1 ? v.y : v.z);
+}
+template <int A, int U, int W, class R>
+__device__ __forceinline__ bool aquad_t(const R* f, V<R> o, V<R> d, R tmin, R tmax, R& t) {
+  R th = fdiv(f[0] - comp<A>(o), comp<A>(d));
+  if (!(tmin <= th && th <= tmax)) return false;
+  R pu = (comp<U>(o) + th * comp<U>(d)) - f[1];
+  R pv = (comp<W>(o) + th * comp<W>(d)) - f[2];
+  R a, b;
+  if constexpr (sizeof(R) == 8) {
+    a = pu / f[5];
+    b = pv / f[6];
+  } else {
+    a = pu * f[3];
+    b = pv * f[4];
+  }
+  if (!(R(0) <= a && a <= R(1) && R(0) <= b && b <= R(1))) return false;
+  t = th;
+  return true;
+}
+template <class R>
+__device__ __forceinline__ bool lin_quad_t(const LinRec<R>& r, V<R> o, V<R> d, R tmin, R tmax, R& t) {
+  switch (r.aux) {
+    case 1: return aquad_t<2, 0, 1>(r.f, o, d, tmin, tmax, t);
+    case 2: return aquad_t<1, 0, 2>(r.f, o, d, tmin, tmax, t);
+    case 3: return aquad_t<2, 1, 0>(r.f, o, d, tmin, tmax, t);
+    case 4: return aquad_t<0, 1, 2>(r.f, o, d, tmin, tmax, t);
+    case 5: return aquad_t<1, 2, 0>(r.f, o, d, tmin, tmax, t);
+    case 6: return aquad_t<0, 2, 1>(r.f, o, d, tmin, tmax, t);
+    default: break;
+  }
+  // general quad: the fields of Quad<R> (quad.h:30-52)
+  V<R> n = ld3(r.f);
+  R th = fdiv(r.f[3] - dot(n, o), dot(n, d));
+  if (!(tmin <= th && th <= tmax)) return false;
+  V<R> p = (o + th * d) - ld3(r.f + 4);
+  R a = dot(p, ld3(r.f + 7)), b = dot(p, ld3(r.f + 10));
+  if (!(R(0) <= a && a <= R(1) && R(0) <= b && b <= R(1))) return false;
+  t = th;
+  return true;
 }
 
 // Closest hit over a primitive list (refs until END); used for volume boundaries.
@@ -328,10 +450,10 @@ __device__ bool volume_t(const DevScene<R>& sc, const Volume<R>& v, V<R> wo, V<R
   if (t1 < R(0)) t1 = R(0);
   R rl = len(d);
   R inside = (t2 - t1) * rl;
-  R u = to_unit<R>(draw_u32(k.ka, k.kb, dim_volume(bounce, jv++)));
-  R hd = v.neg_inv_density * log(u);
+  R u = to_unit<R>(draw_u32(k.ks, dim_volume(bounce, jv++)));
+  R hd = v.neg_inv_density * flog(u);
   if (hd > inside) return false;
-  t = t1 + hd / rl;
+  t = t1 + fdiv(hd, rl);
   return true;
 }
 
@@ -461,16 +583,26 @@ __device__ __forceinline__ void trace_linear(const DevScene<R>& sc, V<R> wo, V<R
   i_best = -1;
   const uint32_t n = sc.n_linear;
   for (uint32_t k = 0; k < n; k++) {
-    const uint32_t op = sc.linear[k];
+    const LinRec<R>& rec = sc.lin[k];
+    const uint32_t op = rec.op;
     const uint32_t ty = etype(op), idx = epay(op);
     R th;
     bool h = false;
     if (ty == E_QUAD) {
-      if (!(op == excl_e && cur == excl_i)) h = quad_t(sc.quads[idx], o, d, tmin, tmax, th);
+      if (!(op == excl_e && cur == excl_i)) h = lin_quad_t(rec, o, d, tmin, tmax, th);
     } else if (SPH && ty == E_SPHERE) {
-      h = sphere_t(sc.spheres[idx], o, d, time, tmin, tmax, op == excl_e && cur == excl_i, th);
+      h = sphere_test(ld3(rec.f), ld3(rec.f + 4), rec.f[3], rec.aux != 0, o, d, time, tmin, tmax,
+                      op == excl_e && cur == excl_i, th);
     } else if (TRI && ty == E_TRI) {
-      if (!(op == excl_e && cur == excl_i)) h = tri_t(sc.tris[idx], o, d, tmin, tmax, th);
+      if (!(op == excl_e && cur == excl_i)) {
+        Tri<R> tr;
+        for (int q = 0; q < 3; q++) {
+          tr.p0[q] = rec.f[q];
+          tr.e1[q] = rec.f[3 + q];
+          tr.e2[q] = rec.f[6 + q];
+        }
+        h = tri_t(tr, o, d, tmin, tmax, th);
+      }
     } else if (ty == E_INSTANCE) {
       cur = (int32_t)idx;
       o = wo;
@@ -526,16 +658,18 @@ __device__ __forceinline__ V<R> onb_transform(const Onb<R>& b, V<R> v) {  // onb
 template <class R>
 __device__ __forceinline__ V<R> on_sphere(R u1, R u2) {
   R cos_theta = R(1) - R(2) * u1;
-  R sin_theta = sqrt(R(1) - cos_theta * cos_theta);
-  R phi = R(2) * Num<R>::pi() * u2;
-  return mkv(sin_theta * cos(phi), cos_theta, sin_theta * sin(phi));
+  R sin_theta = fsqrt(R(1) - cos_theta * cos_theta);
+  R sp, cp;
+  sincos2pi(u2, sp, cp);
+  return mkv(sin_theta * cp, cos_theta, sin_theta * sp);
 }
 // random_cosine_direction (utility.h:61-69)
 template <class R>
 __device__ __forceinline__ V<R> cosine_dir(R r1, R r2) {
-  R phi = R(2) * Num<R>::pi() * r1;
-  R sr2 = sqrt(r2);
-  return mkv(cos(phi) * sr2, sqrt(R(1) - r2), sin(phi) * sr2);
+  R sp, cp;
+  sincos2pi(r1, sp, cp);
+  R sr2 = fsqrt(r2);
+  return mkv(cp * sr2, fsqrt(R(1) - r2), sp * sr2);
 }
 
 // hittable_pdf over the light (hittable_list.h:39-50 -> quad.h:66-78 / sphere.h:76-81 / hittable.h:39-41)
@@ -546,11 +680,11 @@ __device__ __forceinline__ R light_pdf(const Light<R>& L, V<R> o, V<R> dir) {
     if (!quad_t(L.quad, o, dir, R(0.001), Num<R>::inf(), t)) return R(0);
     R dist2 = t * t * dot(dir, dir);
     R cosine = fabs(dot(unit(dir), ld3(L.quad.n)));
-    return dist2 / (cosine * L.quad.area);
+    return fdiv(dist2, cosine * L.quad.area);
   }
   if (L.kind == L_SPHERE) {
     V<R> f = o - ld3(L.center);
-    return L.radius * L.radius * Num<R>::pi() / dot(f, f);
+    return fdiv(L.radius * L.radius * Num<R>::pi(), dot(f, f));
   }
   return R(0);
 }

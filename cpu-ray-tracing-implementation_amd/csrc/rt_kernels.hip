@@ -56,8 +56,9 @@ struct alignas(4 * sizeof(R)) R4 {
 // or 32-byte (fp64) records so every access is a coalesced dwordx4:
 //   O  origin, ray time            D  direction, bounce (-1: slot retired)
 //   T  throughput                  L  radiance of the running sample
-//   A  running sum of the item     S  key_pixel, key_sample, item, sample
-//   X  the surface the ray leaves (entry, instance): self-intersection exclusion
+//   A  running sum of the item     S  key_pixel, key of the running sample, item, sample
+//   X  the surface the ray leaves (entry, instance): self-intersection exclusion;
+//      the pixel (x | y << 16) and the end of the sample range of the slot's item
 template <class R>
 struct Params {
   DevScene<R> sc;
@@ -67,7 +68,7 @@ struct Params {
   R4<R>* L;
   R4<R>* A;
   uint4* S;
-  uint2* X;
+  uint4* X;
   R* partial;              // per item: 3 sums
   const uint32_t* pixmap;  // local pixel -> global pixel id y*W + x
   const uint32_t* queue;   // live slots, or null = slots [0, n)
@@ -76,6 +77,7 @@ struct Params {
   int32_t max_depth;
   uint64_t seed;
   V<R> pos, du, dv, dir00;
+  V<double> cdu, cdv, cdir00;  // the same in fp64: the fp32 path builds camera rays in fp64 and rounds once
   unsigned long long* seg_shards;
   int32_t K;  // segments per launch
 };
@@ -85,16 +87,17 @@ struct Path {
   V<R> o, d, thr, rad, acc;
   R tm;
   int32_t bounce;
-  uint32_t ka, kb, item, sample;
+  uint32_t ka, ks, item, sample;
   uint32_t xe;
   int32_t xi;
+  uint32_t xy, send;
 };
 
 template <class R>
 __device__ __forceinline__ void load_path(const Params<R>& p, uint32_t slot, R4<R> Dv, Path<R>& s) {
   R4<R> Ov = p.O[slot], Tv = p.T[slot], Lv = p.L[slot], Av = p.A[slot];
   uint4 S = p.S[slot];
-  uint2 X = p.X[slot];
+  uint4 X = p.X[slot];
   s.o = mkv(Ov.x, Ov.y, Ov.z);
   s.tm = Ov.w;
   s.d = mkv(Dv.x, Dv.y, Dv.z);
@@ -103,11 +106,13 @@ __device__ __forceinline__ void load_path(const Params<R>& p, uint32_t slot, R4<
   s.rad = mkv(Lv.x, Lv.y, Lv.z);
   s.acc = mkv(Av.x, Av.y, Av.z);
   s.ka = S.x;
-  s.kb = S.y;
+  s.ks = S.y;
   s.item = S.z;
   s.sample = S.w;
   s.xe = X.x;
   s.xi = (int32_t)X.y;
+  s.xy = X.z;
+  s.send = X.w;
 }
 
 template <class R>
@@ -118,24 +123,40 @@ __device__ __forceinline__ void store_path(const Params<R>& p, uint32_t slot, co
   p.T[slot] = {s.thr.x, s.thr.y, s.thr.z, R(0)};
   p.L[slot] = {s.rad.x, s.rad.y, s.rad.z, R(0)};
   p.A[slot] = {s.acc.x, s.acc.y, s.acc.z, R(0)};
-  p.S[slot] = make_uint4(s.ka, s.kb, s.item, s.sample);
-  p.X[slot] = make_uint2(s.xe, (uint32_t)s.xi);
+  p.S[slot] = make_uint4(s.ka, s.ks, s.item, s.sample);
+  p.X[slot] = make_uint4(s.xe, (uint32_t)s.xi, s.xy, s.send);
 }
 
-// camera::generate_ray, perspective mode (camera.h:244-251,293): a new sample of the slot's item
+// A new work item for the slot: its pixel and that pixel's RNG key.
 template <class R>
-__device__ __forceinline__ void begin_sample(const Params<R>& p, Path<R>& s, uint32_t item, uint32_t sample) {
-  uint32_t gpix = p.pixmap[item % p.npix];
+__device__ __forceinline__ void begin_item(const Params<R>& p, Path<R>& s, uint32_t item) {
+  const uint32_t chunk = item / p.npix;
+  const uint32_t gpix = p.pixmap[item - chunk * p.npix];
   s.item = item;
-  s.sample = sample;
+  s.sample = chunk * p.chunk;
+  s.send = min(s.sample + p.chunk, p.spp);
+  s.xy = (gpix % p.W) | ((gpix / p.W) << 16);
   s.ka = key_pixel(p.seed, gpix);
-  s.kb = key_sample(p.seed, p.first_sample + sample);
-  uint32_t x = gpix % p.W, y = gpix / p.W;
-  V<R> rd = (p.dir00 + R(x) * p.du) + R(y) * p.dv;
-  R ox = to_unit<R>(draw_u32(s.ka, s.kb, 0)) - R(0.5);
-  R oy = to_unit<R>(draw_u32(s.ka, s.kb, 1)) - R(0.5);
-  s.d = (rd + ox * p.du) + oy * p.dv;
-  s.tm = to_unit<R>(draw_u32(s.ka, s.kb, 2));
+}
+
+// camera::generate_ray, perspective mode (camera.h:244-251,293): sample s.sample of the slot's pixel
+template <class R>
+__device__ __forceinline__ void begin_sample(const Params<R>& p, Path<R>& s) {
+  s.ks = key_path(s.ka, key_sample(p.seed, p.first_sample + s.sample));
+  uint32_t x = s.xy & 0xFFFFu, y = s.xy >> 16;
+  R ox = to_unit<R>(draw_u32(s.ks, 0)) - R(0.5);  // exact in fp32 and fp64
+  R oy = to_unit<R>(draw_u32(s.ks, 1)) - R(0.5);
+  if constexpr (sizeof(R) == 4) {
+    // the correctly rounded fp64 direction: a few ulp less error on every camera ray, which
+    // otherwise shows up as paths that cross a checker line or sphere edge differently
+    V<double> rd = (p.cdir00 + double(x) * p.cdu) + double(y) * p.cdv;
+    V<double> dd = (rd + double(ox) * p.cdu) + double(oy) * p.cdv;
+    s.d = mkv(float(dd.x), float(dd.y), float(dd.z));
+  } else {
+    V<R> rd = (p.dir00 + R(x) * p.du) + R(y) * p.dv;
+    s.d = (rd + ox * p.du) + oy * p.dv;
+  }
+  s.tm = to_unit<R>(draw_u32(s.ks, 2));
   s.o = p.pos;
   s.bounce = 0;
   s.thr = mkv(R(1), R(1), R(1));
@@ -154,7 +175,8 @@ __global__ __launch_bounds__(kBlock) void k_init(Params<R> p) {
     s.d = mkv(R(0), R(0), R(0));
     s.bounce = -1;
   } else {
-    begin_sample(p, s, slot, (slot / p.npix) * p.chunk);
+    begin_item(p, s, slot);
+    begin_sample(p, s);
   }
   store_path(p, slot, s);
 }
@@ -172,6 +194,10 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
   const V<R> o = s.o, d = s.d;
 
   if (e == kNoHit) {  // camera::miss (camera.h:180-190)
+#ifdef RT_DEBUG_TRACE
+    printf("[dev] bounce %d o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) miss\n", s.bounce, (double)o.x, (double)o.y,
+           (double)o.z, (double)d.x, (double)d.y, (double)d.z);
+#endif
     if (sc.background >= 0) {
       R tb;
       if (sphere_roots<R>(o.x, o.y, o.z, d.x, d.y, d.z, o.x, o.y, o.z, R(1), R(0.001), Num<R>::inf(), false, tb)) {
@@ -205,7 +231,27 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
         mat = q.mat;
       } else if (ty == E_SPHERE) {  // sphere.h:69 (center_ member; (0,0,0) for moving spheres)
         const Sphere<R>& sp = sc.spheres[idx];
-        outward = (po - ld3(sp.cn)) / sp.r;
+        if constexpr (sizeof(R) == 8) {
+          outward = (po - ld3(sp.cn)) / sp.r;
+        } else {
+          if (sp.r > R(16)) {
+            // Big spheres (intersected in fp64, see sphere_test): o + t*d in fp32 is off the
+            // surface by ~1e-7 absolute, enough to flip the sign of y near the top of the RTOW
+            // ground (y = 0 under the glass sphere) and with it the checker parity
+            // (texture.h:51-55). Rebuild the point on the sphere in fp64, then round.
+            double cx = sp.c1[0], cy = sp.c1[1], cz = sp.c1[2];
+            if (sp.moving) {
+              cx += (double)s.tm * sp.dc[0];
+              cy += (double)s.tm * sp.dc[1];
+              cz += (double)s.tm * sp.dc[2];
+            }
+            double vx = (double)oo.x + (double)t * dd.x - cx, vy = (double)oo.y + (double)t * dd.y - cy,
+                   vz = (double)oo.z + (double)t * dd.z - cz;
+            double k = (double)sp.r / sqrt(vx * vx + vy * vy + vz * vz);
+            po = mkv((float)(cx + vx * k), (float)(cy + vy * k), (float)(cz + vz * k));
+          }
+          outward = (po - ld3(sp.cn)) * fdiv(R(1), sp.r);
+        }
         mat = sp.mat;
       } else {
         const Tri<R>& tr = sc.tris[idx];
@@ -222,6 +268,12 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
         }
       }
     }
+#ifdef RT_DEBUG_TRACE  // development build (scripts/dev_sample_trace.py): one line per segment
+    printf("[dev] bounce %d o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) t=%.9g p=(%.9g %.9g %.9g) n=(%.9g %.9g %.9g) "
+           "front=%d mat=%d ty=%u idx=%u\n", s.bounce, (double)o.x, (double)o.y, (double)o.z, (double)d.x, (double)d.y,
+           (double)d.z, (double)t, (double)pw.x, (double)pw.y, (double)pw.z, (double)n.x, (double)n.y, (double)n.z,
+           (int)front, sc.mats[mat].kind, ty, idx);
+#endif
     const Material<R>& m = sc.mats[mat];
     if (m.kind == M_DIFFUSE_LIGHT) {  // material.h:211-215; no scatter
       if (front) {
@@ -233,7 +285,7 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
       V<R> att = tex_sample(sc.texs[m.tex], pw);
       const uint32_t bounce = (uint32_t)s.bounce;
       uint32_t js = 0;
-      auto U = [&]() { return to_unit<R>(draw_u32(s.ka, s.kb, dim_scatter(bounce, js++))); };
+      auto U = [&]() { return to_unit<R>(draw_u32(s.ks, dim_scatter(bounce, js++))); };
       if (m.kind == M_METAL) {  // material.h:85-92
         V<R> dir = unit(reflect(d, n));
         R u1 = U();
@@ -241,14 +293,14 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
         new_d = dir + m.fuzz * unit(on_sphere(u1, u2));
         s.thr = s.thr * att;
       } else if (m.kind == M_DIELECTRIC) {  // material.h:113-131
-        R ri = front ? (R(1) / m.refr) : m.refr;
+        R ri = front ? fdiv(R(1), m.refr) : m.refr;
         V<R> ud = unit(d);
         R cos_t = fmin(dot(-ud, n), R(1));
-        R sin_t = sqrt(R(1) - cos_t * cos_t);
+        R sin_t = fsqrt(R(1) - cos_t * cos_t);
         bool cant = ri * sin_t > R(1);
-        R r0 = (R(1) - ri) / (R(1) + ri);
+        R r0 = fdiv(R(1) - ri, R(1) + ri);
         r0 = r0 * r0;
-        if (cant || (r0 + (R(1) - r0) * pow(R(1) - cos_t, R(5))) > U())
+        if (cant || (r0 + (R(1) - r0) * pow5(R(1) - cos_t)) > U())
           new_d = reflect(ud, n);
         else
           new_d = refract(ud, n, ri);
@@ -265,7 +317,7 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
           R u1 = U();
           R u2 = U();
           dir = iso ? unit(on_sphere(u1, u2)) : onb_transform(b, cosine_dir(u1, u2));
-          pv = iso ? iso_pdf : fmax(R(0), dot(unit(dir), b.y) / Num<R>::pi());
+          pv = iso ? iso_pdf : fmax(R(0), fdiv(dot(unit(dir), b.y), Num<R>::pi()));
         } else {  // dual_pdf(hittable_pdf(light), material pdf) (camera.h:227-239, pdf.h:48-61)
           R c = U();
           R u1 = U();
@@ -274,7 +326,7 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
             dir = light_random(Lt, pw, u1, u2);
           else
             dir = iso ? unit(on_sphere(u1, u2)) : onb_transform(b, cosine_dir(u1, u2));
-          R mp = iso ? iso_pdf : fmax(R(0), dot(unit(dir), b.y) / Num<R>::pi());
+          R mp = iso ? iso_pdf : fmax(R(0), fdiv(dot(unit(dir), b.y), Num<R>::pi()));
           pv = R(0.5) * light_pdf(Lt, pw, dir) + R(0.5) * mp;
         }
         R ps;
@@ -282,9 +334,12 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
           ps = iso_pdf;
         } else {
           R c = dot(n, unit(dir));
-          ps = c < R(0) ? R(0) : c / Num<R>::pi();
+          ps = c < R(0) ? R(0) : fdiv(c, Num<R>::pi());
         }
-        s.thr = s.thr * ((att * ps) / pv);
+        if constexpr (sizeof(R) == 8)
+          s.thr = s.thr * ((att * ps) / pv);  // camera.h:238 grouping on the parity path
+        else
+          s.thr = s.thr * (att * fdiv(ps, pv));
         new_d = dir;
       }
       new_o = pw;
@@ -303,22 +358,20 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
   }
   // the sample is finished (camera.h:167): add it to the item's running sum
   s.acc = s.acc + s.rad;
-  uint32_t item = s.item, sample = s.sample + 1;
-  uint32_t chunk_end = min((item / p.npix) * p.chunk + p.chunk, p.spp);
-  if (sample >= chunk_end) {
-    R* dst = p.partial + 3ull * item;
+  s.sample += 1;
+  if (s.sample >= s.send) {
+    R* dst = p.partial + 3ull * s.item;
     dst[0] = s.acc.x;
     dst[1] = s.acc.y;
     dst[2] = s.acc.z;
     s.acc = mkv(R(0), R(0), R(0));
-    item += p.P;
-    if (item >= p.n_items) {
+    if (s.item + p.P >= p.n_items) {
       s.bounce = -1;
       return false;
     }
-    sample = (item / p.npix) * p.chunk;
+    begin_item(p, s, s.item + p.P);
   }
-  begin_sample(p, s, item, sample);
+  begin_sample(p, s);
   return true;
 }
 
@@ -373,7 +426,7 @@ __global__ __launch_bounds__(kBlock) void k_step(Params<R> p) {
       R t;
       uint32_t e;
       int32_t inst;
-      Trav::run(p.sc, s, Keys{s.ka, s.kb}, stk.v + threadIdx.x, t, e, inst);
+      Trav::run(p.sc, s, Keys{s.ks}, stk.v + threadIdx.x, t, e, inst);
       segs++;
       if (!shade(p, s, t, e, inst)) break;
     }
@@ -593,7 +646,7 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
   s.mats = (const Material<R>*)at(h.off_mats);
   s.texs = (const Texture<R>*)at(h.off_texs);
   s.light = (const Light<R>*)at(h.off_light);
-  s.linear = (const uint32_t*)at(h.off_linear);
+  s.lin = (const LinRec<R>*)at(h.off_linear);
   s.n_linear = h.n_linear;
   s.root = h.root;
   s.background = h.background;
@@ -668,9 +721,9 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     P = std::max<uint32_t>(1, std::min(P, n_items));
     const uint32_t nblk_max = (P + kBlock - 1) / kBlock;
 
-    // path state: 5 R4 arrays (O, D, T, L, A) + uint4 keys (S) + uint2 exclusion (X), each P long
+    // path state: 5 R4 arrays (O, D, T, L, A) + uint4 keys (S) + uint4 exclusion/pixel (X), each P long
     auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
-    const size_t r4 = al(sizeof(R4<R>) * (size_t)P), sb = al(16 * (size_t)P), xb = al(8 * (size_t)P);
+    const size_t r4 = al(sizeof(R4<R>) * (size_t)P), sb = al(16 * (size_t)P), xb = al(16 * (size_t)P);
     if ((s = ensure(c, c->state, 5 * r4 + sb + xb)) != RT_OK) return s;
     if ((s = ensure(c, c->partial, 3ull * n_items * sizeof(R))) != RT_OK) return s;
     if ((s = ensure(c, c->pixmap, 4ull * npix)) != RT_OK) return s;
@@ -689,7 +742,7 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     p.L = (R4<R>*)(sp + 3 * r4);
     p.A = (R4<R>*)(sp + 4 * r4);
     p.S = (uint4*)(sp + 5 * r4);
-    p.X = (uint2*)(sp + 5 * r4 + sb);
+    p.X = (uint4*)(sp + 5 * r4 + sb);
     p.partial = (R*)c->partial.ptr;
     p.pixmap = (const uint32_t*)c->pixmap.ptr;
     p.queue = nullptr;
@@ -708,6 +761,9 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     p.du = tov<R>(vw.du);
     p.dv = tov<R>(vw.dv);
     p.dir00 = tov<R>(vw.dir00);
+    p.cdu = tov<double>(vw.du);
+    p.cdv = tov<double>(vw.dv);
+    p.cdir00 = tov<double>(vw.dir00);
     p.seg_shards = (unsigned long long*)c->counters.ptr;
     const int K = prm->segments_per_launch > 0 ? std::min(prm->segments_per_launch, 64) : kAutoSegments;
     p.K = K;
@@ -940,7 +996,7 @@ rt_status rt_set_timing(rt_context* c, int32_t enable) {
 }
 
 uint32_t rt_rng_u32(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t dim) {
-  return draw_u32(key_pixel(seed, pixel), key_sample(seed, sample), dim);
+  return draw_u32(key_path(key_pixel(seed, pixel), key_sample(seed, sample)), dim);
 }
 
 }  // extern "C"

@@ -50,6 +50,21 @@ constexpr int kMaxBvhDepth = 26; // the builder keeps every BVH within this dept
 constexpr int kLinearMax = 96;
 constexpr uint32_t kInstEnd = kRestoreBase;  // back to the world ray
 
+// One linear-program op with the data its test needs inline, so a wave fetches it
+// with a single scalar load (64 B for fp32, 128 B for fp64).
+//   QUAD, aux = 0        general quad: f = n[3], D, q[3], a[3], b[3] (as Quad)
+//   QUAD, aux = 1 + perm axis-aligned quad (perm 0..5 encodes the plane axis A and
+//                        the axes U, V of u and v): f = q[A], q[U], q[V], 1/u[U], 1/v[V], u[U], v[V]
+//   SPHERE               f = c1[3], r, dc[3]; aux = moving
+//   TRI                  f = p0[3], e1[3], e2[3]
+//   INSTANCE / VOLUME / kInstEnd: no payload (records in insts / vols)
+template <class R>
+struct alignas(16) LinRec {
+  uint32_t op;
+  uint32_t aux;
+  R f[14];
+};
+
 // quad.h:9-23 precomputed: n = unit(cross(u,v)), D = dot(n, corner),
 // a = cross(v, w), b = cross(w, u) with w = cross(u,v)/dot(cross(u,v),cross(u,v)),
 // so alpha = dot(p - corner, a) = dot(w, cross(p - corner, v)) and beta = dot(p - corner, b).
@@ -165,7 +180,7 @@ struct SceneHeader {
   int32_t has_volumes;
   int32_t num_instances;
   uint64_t off_quads, off_spheres, off_tris, off_instances, off_volumes, off_nodes, off_refs, off_mats, off_texs,
-      off_light, off_linear;
+      off_light, off_linear;  // off_linear: LinRec array
   uint64_t bytes;
   uint32_t n_linear;  // 0: no linear program (use the BVH traversal)
   uint32_t pad_;

@@ -180,6 +180,9 @@ class Compiler {
   Item list_of(const std::vector<Item>& items);
   Item bvh(std::vector<Item>& items, size_t b, size_t e, int depth);
   int make_instance(const std::vector<Op>& chain, uint32_t blas);
+  LinRec<double> lin_record(uint32_t op) const;
+  std::vector<int> aligned_;  // per quad: 1 + perm for axis-aligned quads, 0 otherwise
+  std::vector<double> qu_, qv_;  // per quad: u[U], v[V] (aligned quads)
   void light_from(int idx);
 };
 
@@ -204,6 +207,25 @@ Item Compiler::prim_item(const rt_object& o) {
     q.mat = o.material;
     quads_.push_back(q);
     it.entry = mk(E_QUAD, (uint32_t)quads_.size() - 1);
+    // axis-aligned: u and v each along one axis, on different axes (then n is exactly +-e_A)
+    auto single_axis = [](const double* v) {
+      int k = -1;
+      for (int j = 0; j < 3; j++)
+        if (v[j] != 0.0) {
+          if (k >= 0) return -1;
+          k = j;
+        }
+      return k;
+    };
+    int U = single_axis(o.b), Vv = single_axis(o.c);
+    int perm = -1;
+    if (U >= 0 && Vv >= 0 && U != Vv) {
+      static const int kPerm[3][3] = {{-1, 0, 1}, {2, -1, 3}, {4, 5, -1}};  // (U, V) -> perm
+      perm = kPerm[U][Vv];
+    }
+    aligned_.push_back(perm + 1);
+    qu_.push_back(U >= 0 ? o.b[U] : 0.0);
+    qv_.push_back(Vv >= 0 ? o.c[Vv] : 0.0);
     double c1[3], c2[3], c3[3];
     for (int k = 0; k < 3; k++) {
       c1[k] = o.a[k] + o.b[k];
@@ -544,6 +566,9 @@ void Compiler::light_from(int idx) {
     light_.kind = L_QUAD;
     light_.quad = quads_.back();
     quads_.resize(before);
+    aligned_.resize(before);
+    qu_.resize(before);
+    qv_.resize(before);
     for (int k = 0; k < 3; k++) {
       light_.u[k] = o->b[k];
       light_.v[k] = o->c[k];
@@ -633,6 +658,13 @@ Node<float> to32(const Node<double>& n) {
   return r;
 }
 Material<float> to32(const Material<double>& m) { return {m.kind, m.tex, (float)m.fuzz, (float)m.refr}; }
+LinRec<float> to32(const LinRec<double>& l) {
+  LinRec<float> r{};
+  r.op = l.op;
+  r.aux = l.aux;
+  for (int k = 0; k < 14; k++) r.f[k] = (float)l.f[k];
+  return r;
+}
 Texture<float> to32(const Texture<double>& t) {
   Texture<float> r{};
   cvt3(r.c0, t.c0);
@@ -659,11 +691,11 @@ auto map32(const std::vector<T>& v) {
   return r;
 }
 
-template <class Q, class S, class T, class I, class V, class N, class M, class X, class L>
+template <class Q, class S, class T, class I, class V, class N, class M, class X, class L, class LR>
 SceneHeader pack(std::vector<unsigned char>& blob, const std::vector<Q>& q, const std::vector<S>& s,
                  const std::vector<T>& t, const std::vector<I>& in, const std::vector<V>& vo, const std::vector<N>& nd,
                  const std::vector<uint32_t>& refs, const std::vector<M>& m, const std::vector<X>& x, const L& light,
-                 const std::vector<uint32_t>& linear) {
+                 const std::vector<LR>& linear) {
   SceneHeader h{};
   blob.clear();
   h.off_quads = append(blob, q);
@@ -690,6 +722,54 @@ SceneHeader pack(std::vector<unsigned char>& blob, const std::vector<Q>& q, cons
   h.n_texs = (uint32_t)x.size();
   h.num_instances = (int32_t)in.size();
   return h;
+}
+
+// perm -> (A, U, V): the plane axis and the axes of u and v (rt_scene.h LinRec)
+constexpr int kPermAxes[6][3] = {{2, 0, 1}, {1, 0, 2}, {2, 1, 0}, {0, 1, 2}, {1, 2, 0}, {0, 2, 1}};
+
+LinRec<double> Compiler::lin_record(uint32_t op) const {
+  LinRec<double> r{};
+  r.op = op;
+  const uint32_t ty = etype(op), i = epay(op);
+  if (op == kInstEnd || ty == E_INSTANCE || ty == E_VOLUME) return r;
+  if (ty == E_QUAD) {
+    const Quad<double>& q = quads_[i];
+    if (aligned_[i]) {
+      const int* ax = kPermAxes[aligned_[i] - 1];
+      r.aux = (uint32_t)aligned_[i];
+      r.f[0] = q.q[ax[0]];
+      r.f[1] = q.q[ax[1]];
+      r.f[2] = q.q[ax[2]];
+      r.f[3] = 1.0 / qu_[i];
+      r.f[4] = 1.0 / qv_[i];
+      r.f[5] = qu_[i];
+      r.f[6] = qv_[i];
+    } else {
+      for (int k = 0; k < 3; k++) {
+        r.f[k] = q.n[k];
+        r.f[4 + k] = q.q[k];
+        r.f[7 + k] = q.a[k];
+        r.f[10 + k] = q.b[k];
+      }
+      r.f[3] = q.D;
+    }
+  } else if (ty == E_SPHERE) {
+    const Sphere<double>& sp = spheres_[i];
+    for (int k = 0; k < 3; k++) {
+      r.f[k] = sp.c1[k];
+      r.f[4 + k] = sp.dc[k];
+    }
+    r.f[3] = sp.r;
+    r.aux = (uint32_t)sp.moving;
+  } else if (ty == E_TRI) {
+    const Tri<double>& t = tris_[i];
+    for (int k = 0; k < 3; k++) {
+      r.f[k] = t.p0[k];
+      r.f[3 + k] = t.e1[k];
+      r.f[6 + k] = t.e2[k];
+    }
+  }
+  return r;
 }
 
 bool Compiler::run(CompiledScene* out, std::string* err) {
@@ -757,14 +837,15 @@ bool Compiler::run(CompiledScene* out, std::string* err) {
   }
   Item lin_top;
   join_lin(lin_top, top);
-  std::vector<uint32_t> linear;
-  if (lin_top.lin_ok) linear = lin_top.lin;
+  std::vector<LinRec<double>> linear;
+  if (lin_top.lin_ok)
+    for (uint32_t op : lin_top.lin) linear.push_back(lin_record(op));
   out->stack_need = std::max(1, root.need);
   out->bvh_depth = root.depth;
   out->num_items = (int)top.size();
   out->hdr64 = pack(out->blob64, quads_, spheres_, tris_, insts_, vols_, nodes_, refs_, mats_, texs_, light_, linear);
   out->hdr = pack(out->blob32, map32(quads_), map32(spheres_), map32(tris_), map32(insts_), map32(vols_),
-                  map32(nodes_), refs_, map32(mats_), map32(texs_), to32(light_), linear);
+                  map32(nodes_), refs_, map32(mats_), map32(texs_), to32(light_), map32(linear));
   for (SceneHeader* h : {&out->hdr, &out->hdr64}) {
     h->root = root.entry;
     h->background = d_->background;

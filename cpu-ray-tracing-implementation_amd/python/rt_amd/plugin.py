@@ -41,6 +41,7 @@ class ConfigScene:
         if not self._h:
             raise RuntimeError(f"rtsc_build({name}): {err.value.decode()}")
         self.spp, self.max_depth = spp.value, depth.value
+        self.desc._owner = self  # the descriptor points into memory this handle owns
 
     def __del__(self):
         if getattr(self, "_h", None) and _lib is not None:

@@ -73,7 +73,9 @@ inline uint32_t key_pixel(uint64_t seed, uint32_t pixel) {
 inline uint32_t key_sample(uint64_t seed, uint32_t sample) {
   return mix32(sample + mix32((uint32_t)(seed >> 32) + 0x7F4A7C15u));
 }
-inline uint32_t draw_u32(uint32_t ka, uint32_t kb, uint32_t dim) { return mix32(ka ^ mix32(kb + dim * 0x9E3779B9u)); }
+// the key of one camera sample (pixel, sample); a draw is one more mix of key + dim * phi
+inline uint32_t key_path(uint32_t ka, uint32_t kb) { return mix32(ka ^ kb); }
+inline uint32_t draw_u32(uint32_t ks, uint32_t dim) { return mix32(ks + dim * 0x9E3779B9u); }
 inline double to_unit(uint32_t x) { return (double)(x >> 8) * (1.0 / 16777216.0); }
 
 // Draw-dimension layout per camera sample (counter mode):
@@ -84,10 +86,10 @@ enum { kDimsCamera = 3, kDimsPerBounce = 16, kVolumeSlots = 12 };
 
 struct rngctx {
   int mode = ORC_RNG_COUNTER;
-  uint32_t ka = 0, kb = 0;
+  uint32_t ks = 0;  // key_path(key_pixel, key_sample)
   uint32_t bounce = 0, jv = 0, js = 0;
   double glibc() const { return std::rand() / (RAND_MAX + 1.0); }  // utility.h:20
-  double at(uint32_t dim) const { return to_unit(draw_u32(ka, kb, dim)); }
+  double at(uint32_t dim) const { return to_unit(draw_u32(ks, dim)); }
   double camera(int k) const { return mode == ORC_RNG_COMPAT ? glibc() : at((uint32_t)k); }
   double volume() {
     if (mode == ORC_RNG_COMPAT) return glibc();
@@ -208,6 +210,9 @@ struct otex {
 };
 
 // ---------------------------------------------------------------- hit record (hittable.h:7-30)
+// development aid: orc_set_trace(1) prints every segment of single-threaded renders to stderr
+static int g_trace = 0;
+
 struct omat;
 struct hrec {
   v3 p, n;
@@ -747,7 +752,15 @@ struct integrator {
     g.next_bounce((uint32_t)(max_depth - iteration));
     segments++;
     hrec rec;
-    if (!sc->world->hit(r, ivl(0.001, kInf), rec, g)) return miss(r, g);
+    if (!sc->world->hit(r, ivl(0.001, kInf), rec, g)) {
+      if (g_trace) std::fprintf(stderr, "[trace] bounce %d o=(%.17g %.17g %.17g) d=(%.17g %.17g %.17g) miss\n",
+                                max_depth - iteration, r.o.x, r.o.y, r.o.z, r.d.x, r.d.y, r.d.z);
+      return miss(r, g);
+    }
+    if (g_trace)
+      std::fprintf(stderr, "[trace] bounce %d o=(%.17g %.17g %.17g) d=(%.17g %.17g %.17g) t=%.17g p=(%.17g %.17g %.17g) "
+                   "n=(%.9g %.9g %.9g) front=%d mat=%d\n", max_depth - iteration, r.o.x, r.o.y, r.o.z, r.d.x, r.d.y,
+                   r.d.z, rec.t, rec.p.x, rec.p.y, rec.p.z, rec.n.x, rec.n.y, rec.n.z, (int)rec.front, rec.mat->kind);
     v3 emission = rec.mat->emitted(rec);
     srec s;
     if (!rec.mat->scatter(r, rec, s, g)) return emission;
@@ -1067,9 +1080,9 @@ inline v3 render_pixel(const job& jb, int x, int y, uint64_t& segs) {  // camera
   v3 sum(0, 0, 0);
   rngctx g;
   g.mode = jb.mode;
-  g.ka = key_pixel(jb.seed, (uint32_t)(y * jb.W + x));
+  uint32_t ka = key_pixel(jb.seed, (uint32_t)(y * jb.W + x));
   for (int k = 0; k < jb.spp; k++) {
-    g.kb = key_sample(jb.seed, (uint32_t)(jb.first + k));
+    g.ks = key_path(ka, key_sample(jb.seed, (uint32_t)(jb.first + k)));
     g.bounce = 0;
     ray3 r = generate_ray(jb.vw, y, x, g);
     sum = sum + it.ray_color(r, jb.depth, g);
@@ -1083,6 +1096,8 @@ inline v3 render_pixel(const job& jb, int x, int y, uint64_t& segs) {  // camera
 using namespace orc;
 
 extern "C" {
+
+void orc_set_trace(int on) { g_trace = on; }
 
 void* orc_scene_from_desc(const rt_scene_desc* d, char* err, int errlen) {
   auto fail = [&](const std::string& m) -> void* {
@@ -1239,7 +1254,7 @@ size_t orc_write_ppm(const double* img, int w, int h, char* buf, size_t cap) {  
 }
 
 uint32_t orc_rng_u32(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t dim) {
-  return draw_u32(key_pixel(seed, pixel), key_sample(seed, sample), dim);
+  return draw_u32(key_path(key_pixel(seed, pixel), key_sample(seed, sample)), dim);
 }
 
 int orc_kat_sphere_hit(const double c[3], double r, const double o[3], const double d[3], double tmin, double tmax,

@@ -68,6 +68,8 @@ size_t orc_write_ppm(const double* image, int width, int height, char* buf, size
 
 /* The counter RNG: 32-bit draw for (seed, pixel, sample, dim). */
 uint32_t orc_rng_u32(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t dim);
+/* Development aid: 1 = print every traced segment to stderr (use with threads = 1). */
+void orc_set_trace(int on);
 
 /* Scalar building blocks exposed for known-answer tests. out[] sizes noted. */
 int orc_kat_sphere_hit(const double c[3], double r, const double o[3], const double d[3], double tmin,

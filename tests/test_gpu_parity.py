@@ -80,9 +80,26 @@ def test_fp32_rtow_statistics(ctx):
     # paths for a few samples; the image statistics still agree with the oracle
     desc, cam, _, _ = scenes.rtow(width=96, aspect=1.5)
     img, ref, _ = render_both(ctx, desc, cam, 16, 50, 3, F32)
-    np.testing.assert_allclose(img.reshape(-1, 3).mean(0), ref.reshape(-1, 3).mean(0), rtol=5e-3)
-    assert np.mean(np.abs(img - ref).max(-1) > 0.05) < 0.02
-    assert (rmse(img, ref) < 1e-2).all()
+    np.testing.assert_allclose(img.reshape(-1, 3).mean(0), ref.reshape(-1, 3).mean(0), rtol=1e-3)
+    assert np.mean(np.abs(img - ref).max(-1) > 1e-3) < 0.005
+    assert (rmse(img, ref) < 2e-3).all(), rmse(img, ref)
+
+
+@pytest.mark.parametrize("name,w,a,spp,depth,limit", [
+    ("three_material_ball", 200, 1.5, 16, 10, 2e-4),
+    ("cornell_box", 200, 1.0, 16, 10, 5e-5),
+    ("cornell_box_with_volume", 160, 1.0, 16, 10, 8e-5),
+], ids=["three_material_ball", "cornell_box", "cornell_box_with_volume"])
+def test_fp32_divergent_samples_are_rare(ctx, name, w, a, spp, depth, limit):
+    # fp32 follows the fp64 path sample for sample except where rounding moves a ray across
+    # an edge or a checker line. A pixel with a divergent sample differs by ~value/spp, so
+    # count those pixels: an fp32 accuracy loss (e.g. a cancelling ray/sphere quadratic,
+    # rt_device.h sphere_roots) shows up here as tens of pixels instead of a handful.
+    desc, cam, _, _ = scenes.SCENES[name](width=w, aspect=a)
+    img, ref, _ = render_both(ctx, desc, cam, spp, depth, 7, F32)
+    d = np.abs(img - ref).max(-1)
+    assert np.mean(d > 1e-3) < limit, (int((d > 1e-3).sum()), d.size)
+    assert (rmse(img, ref) < 2e-4).all(), rmse(img, ref)
 
 
 @pytest.mark.parametrize("precision", [F32, F64])
