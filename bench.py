@@ -11,6 +11,7 @@ gathers them (RCCL, torch.distributed "nccl") into the full linear framebuffer.
     torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -59,6 +60,23 @@ def cpu_baseline(scene_name, width, aspect, spp, depth, seed, threads):
     return {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": f"oracle (fp64 C++ restatement, counter RNG) on {len(rows)} rows (every {step}th) x "
                       f"{cam.image_width} px x {spp} spp, depth {depth}: {n / 1e6:.1f} Msamples in {dt:.1f} s"}
+
+
+def measured_traffic(workload):
+    """HBM bytes per k_step launch from the newest committed PMC summary of this exact workload
+    (profiles/<round>_traffic.json, written by scripts/pmc_summary.py), or None."""
+    found = None
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json"))):
+        with open(f) as fh:
+            d = json.load(fh)
+        if d.get("workload") == workload:
+            found = (os.path.basename(f), d["bytes_per_launch"])
+    return found
+
+
+def workload_key(scene_name, W, H, spp, depth, args):
+    return (f"{scene_name} {W}x{H} {spp}spp depth {depth} {args.precision} pool={args.pool} chunk={args.chunk} "
+            f"K={args.segments_per_launch} world={args.gpus}")
 
 
 def main():
@@ -165,11 +183,16 @@ def main():
             alg_bytes = (B_GEN + B_ACC) * my_samples + (B_EXT + B_SHADE) * segs
             avg_s = step_ms / 1e3 / iters
             achieved = alg_bytes / (step_ms / 1e3) / 1e9
+            mt = measured_traffic(workload_key(scene_name, W, H, spp, depth, args))
             roof = {"bound": "hbm", "kernel": "k_step", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": int(mt[1]) if mt else None,
                     "avg_launch_us": round(avg_s * 1e6, 2), "launches": iters,
                     "alg_bytes_per_launch": int(alg_bytes / iters),
                     "kernel_share_of_wall": round(step_ms / 1e3 / elapsed, 4)}
+            if mt:
+                roof["traffic_source"] = "profiles/" + mt[0]
+                roof["traffic_over_alg"] = round(mt[1] / (alg_bytes / iters), 4)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(scene_name, width, aspect, spp, depth, args.seed, args.cpu_threads)
@@ -181,6 +204,7 @@ def main():
             "scaling": "strong", "vs_baseline": None, "dtype": "fp32" if prec == abi.RT_PREC_F32 else "fp64",
             "data": "synthetic (the reference's Cornell Box scene, procedurally built; no assets)",
             "config": {"workload": f"{scene_name} {W}x{H} {spp}spp depth {depth}, light sampling on",
+                       "key": workload_key(scene_name, W, H, spp, depth, args),
                        "image": [W, H], "spp": spp, "max_depth": depth, "tiles": "64x64 round-robin over ranks",
                        "parallelism": f"tiles{world}", "segments_per_sample": round(seg_per_sample, 4),
                        "segments_total": segs_total / args.steps, "kernel_timing": args.kernel_timing,

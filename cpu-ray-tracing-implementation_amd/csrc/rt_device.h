@@ -38,6 +38,16 @@ __device__ __forceinline__ void sincos2pi(float u, float& s, float& c) {
 }
 #endif
 __device__ __forceinline__ double fdiv(double a, double b) { return a / b; }
+// a / b given inv_b = rcp3(..) of b computed once per ray: bit-identical to fdiv(a, b)
+// (fp64 and the precise build divide; rcp3 then returns nothing the compiler keeps)
+__device__ __forceinline__ float fdiv_inv(float a, float b, float inv_b) {
+#ifndef RT_PRECISE_F32
+  return a * inv_b;
+#else
+  return a / b;
+#endif
+}
+__device__ __forceinline__ double fdiv_inv(double a, double b, double) { return a / b; }
 __device__ __forceinline__ double fsqrt(double x) { return sqrt(x); }
 __device__ __forceinline__ double flog(double x) { return log(x); }
 // sin(2*pi*u), cos(2*pi*u); the fp64 form evaluates phi = 2*pi*u first like utility.h:36,64
@@ -362,6 +372,28 @@ __device__ __forceinline__ bool sphere_t(const Sphere<R>& s, V<R> o, V<R> d, R t
   return sphere_test(ld3(s.c1), ld3(s.dc), s.r, s.moving != 0, o, d, time, tmin, tmax, self, t);
 }
 
+// Wave-uniform read through the constant address space: always a scalar load (s_load),
+// which the compiler cannot prove for a loop-carried prefetch from a generic pointer.
+template <class T>
+__device__ __forceinline__ T ld_uniform(const T* p, uint32_t i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  i = __builtin_amdgcn_readfirstlane(i);
+  return ((const __attribute__((address_space(4))) T*)p)[i];
+#else
+  return p[i];  // host pass of a device function: never executed
+#endif
+}
+
+// Per-ray reciprocal direction for fdiv_inv (fp32 fast path only).
+template <class R>
+__device__ __forceinline__ V<R> rcp3(V<R> d) {
+#ifndef RT_PRECISE_F32
+  if constexpr (sizeof(R) == 4)
+    return mkv(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
+#endif
+  return d;
+}
+
 // Axis-aligned quad (rt_scene.h LinRec): n = +-e_A exactly, so quad.h:32-33 reduce to
 // t = (q_A - o_A) / d_A bit for bit; alpha = (p_U - q_U) / u_U, beta = (p_V - q_V) / v_V.
 template <int K, class R>
@@ -369,8 +401,8 @@ __device__ __forceinline__ R comp(V<R> v) {
   return K == 0 ? v.x : (K == 1 ? v.y : v.z);
 }
 template <int A, int U, int W, class R>
-__device__ __forceinline__ bool aquad_t(const R* f, V<R> o, V<R> d, R tmin, R tmax, R& t) {
-  R th = fdiv(f[0] - comp<A>(o), comp<A>(d));
+__device__ __forceinline__ bool aquad_t(const R* f, V<R> o, V<R> d, V<R> inv, R tmin, R tmax, R& t) {
+  R th = fdiv_inv(f[0] - comp<A>(o), comp<A>(d), comp<A>(inv));
   if (!(tmin <= th && th <= tmax)) return false;
   R pu = (comp<U>(o) + th * comp<U>(d)) - f[1];
   R pv = (comp<W>(o) + th * comp<W>(d)) - f[2];
@@ -387,14 +419,14 @@ __device__ __forceinline__ bool aquad_t(const R* f, V<R> o, V<R> d, R tmin, R tm
   return true;
 }
 template <class R>
-__device__ __forceinline__ bool lin_quad_t(const LinRec<R>& r, V<R> o, V<R> d, R tmin, R tmax, R& t) {
+__device__ __forceinline__ bool lin_quad_t(const LinRec<R>& r, V<R> o, V<R> d, V<R> inv, R tmin, R tmax, R& t) {
   switch (r.aux) {
-    case 1: return aquad_t<2, 0, 1>(r.f, o, d, tmin, tmax, t);
-    case 2: return aquad_t<1, 0, 2>(r.f, o, d, tmin, tmax, t);
-    case 3: return aquad_t<2, 1, 0>(r.f, o, d, tmin, tmax, t);
-    case 4: return aquad_t<0, 1, 2>(r.f, o, d, tmin, tmax, t);
-    case 5: return aquad_t<1, 2, 0>(r.f, o, d, tmin, tmax, t);
-    case 6: return aquad_t<0, 2, 1>(r.f, o, d, tmin, tmax, t);
+    case 1: return aquad_t<2, 0, 1>(r.f, o, d, inv, tmin, tmax, t);
+    case 2: return aquad_t<1, 0, 2>(r.f, o, d, inv, tmin, tmax, t);
+    case 3: return aquad_t<2, 1, 0>(r.f, o, d, inv, tmin, tmax, t);
+    case 4: return aquad_t<0, 1, 2>(r.f, o, d, inv, tmin, tmax, t);
+    case 5: return aquad_t<1, 2, 0>(r.f, o, d, inv, tmin, tmax, t);
+    case 6: return aquad_t<0, 2, 1>(r.f, o, d, inv, tmin, tmax, t);
     default: break;
   }
   // general quad: the fields of Quad<R> (quad.h:30-52)
@@ -577,19 +609,21 @@ __device__ __forceinline__ void trace_linear(const DevScene<R>& sc, V<R> wo, V<R
   const R tmin = R(0.001);
   R tmax = Num<R>::inf();
   V<R> o = wo, d = wd;
+  const V<R> winv = rcp3(wd);
+  V<R> inv = winv;
   int32_t cur = -1;
   uint32_t jv = 0;
   e_best = kNoHit;
   i_best = -1;
   const uint32_t n = sc.n_linear;
   for (uint32_t k = 0; k < n; k++) {
-    const LinRec<R>& rec = sc.lin[k];
+    const LinRec<R> rec = ld_uniform(sc.lin, k);  // the whole record into SGPRs at once
     const uint32_t op = rec.op;
     const uint32_t ty = etype(op), idx = epay(op);
     R th;
     bool h = false;
     if (ty == E_QUAD) {
-      if (!(op == excl_e && cur == excl_i)) h = lin_quad_t(rec, o, d, tmin, tmax, th);
+      if (!(op == excl_e && cur == excl_i)) h = lin_quad_t(rec, o, d, inv, tmin, tmax, th);
     } else if (SPH && ty == E_SPHERE) {
       h = sphere_test(ld3(rec.f), ld3(rec.f + 4), rec.f[3], rec.aux != 0, o, d, time, tmin, tmax,
                       op == excl_e && cur == excl_i, th);
@@ -603,17 +637,30 @@ __device__ __forceinline__ void trace_linear(const DevScene<R>& sc, V<R> wo, V<R
         }
         h = tri_t(tr, o, d, tmin, tmax, th);
       }
-    } else if (ty == E_INSTANCE) {
+    } else if (ty == E_INSTANCE) {  // the chain inline in the record (rt_scene.h LinRec)
       cur = (int32_t)idx;
       o = wo;
       d = wd;
-      chain_in(sc.insts[idx], o, d);
+      const uint32_t nops = rec.aux & 7u;
+#pragma unroll
+      for (uint32_t q = 0; q < (uint32_t)kMaxChain; q++) {
+        if (q >= nops) break;
+        XOp<R> x;
+        x.kind = (int32_t)((rec.aux >> (4 + 2 * q)) & 3u);
+        x.x = rec.f[3 * q];
+        x.y = rec.f[3 * q + 1];
+        x.z = rec.f[3 * q + 2];
+        o = op_in(x, o, true);
+        d = op_in(x, d, false);
+      }
+      inv = rcp3(d);
     } else if (VOL && ty == E_VOLUME) {
       h = volume_t(sc, sc.vols[idx], wo, wd, d, time, tmin, tmax, keys, bounce, jv, th);
     } else {  // kInstEnd
       cur = -1;
       o = wo;
       d = wd;
+      inv = winv;
     }
     if (h) {
       tmax = th;

@@ -57,13 +57,16 @@ constexpr uint32_t kInstEnd = kRestoreBase;  // back to the world ray
 //                        the axes U, V of u and v): f = q[A], q[U], q[V], 1/u[U], 1/v[V], u[U], v[V]
 //   SPHERE               f = c1[3], r, dc[3]; aux = moving
 //   TRI                  f = p0[3], e1[3], e2[3]
-//   INSTANCE / VOLUME / kInstEnd: no payload (records in insts / vols)
+//   INSTANCE             the wrapper chain inline: aux = nops | kind_k << (4 + 2k),
+//                        f[3k .. 3k+2] = x, y, z of op k (as XOp; at most kMaxChain = 4)
+//   VOLUME / kInstEnd    no payload (records in vols)
 template <class R>
 struct alignas(16) LinRec {
   uint32_t op;
   uint32_t aux;
   R f[14];
 };
+static_assert(3 * kMaxChain <= 14, "an instance chain must fit one LinRec");
 
 // quad.h:9-23 precomputed: n = unit(cross(u,v)), D = dot(n, corner),
 // a = cross(v, w), b = cross(w, u) with w = cross(u,v)/dot(cross(u,v),cross(u,v)),

@@ -731,7 +731,18 @@ LinRec<double> Compiler::lin_record(uint32_t op) const {
   LinRec<double> r{};
   r.op = op;
   const uint32_t ty = etype(op), i = epay(op);
-  if (op == kInstEnd || ty == E_INSTANCE || ty == E_VOLUME) return r;
+  if (op == kInstEnd || ty == E_VOLUME) return r;
+  if (ty == E_INSTANCE) {
+    const Instance<double>& in = insts_[i];
+    r.aux = (uint32_t)in.nops;
+    for (int k = 0; k < in.nops; k++) {
+      r.aux |= (uint32_t)in.op[k].kind << (4 + 2 * k);
+      r.f[3 * k] = in.op[k].x;
+      r.f[3 * k + 1] = in.op[k].y;
+      r.f[3 * k + 2] = in.op[k].z;
+    }
+    return r;
+  }
   if (ty == E_QUAD) {
     const Quad<double>& q = quads_[i];
     if (aligned_[i]) {

@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Summarise the rocprofv3 passes of scripts/prof_pmc.sh into profiles/.
+
+  python scripts/pmc_summary.py <prof dir> <tag> <workload>
+
+Writes
+  profiles/<tag>_kernel_stats.csv   the --kernel-trace --stats summary (copied as rocprofv3 wrote it)
+  profiles/<tag>_pmc_summary.csv    per kernel and counter: dispatches, mean and total over the run
+  profiles/<tag>_traffic.json       HBM bytes per k_step launch, read by bench.py for roofline.traffic
+
+HBM bytes follow MI355X_MICROARCH.md (HBM [CDNA4]): FETCH_SIZE and WRITE_SIZE are in KiB,
+and on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced read, so
+bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024. FETCH_SIZE and WRITE_SIZE come from
+separate passes (they do not fit one pass), averaged over the same k_step launches.
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short(name):
+    # "void (anonymous namespace)::k_step<float, ...>((anonymous namespace)::Params<float>)" -> "k_step<float, ...>"
+    n = name.replace("(anonymous namespace)::", "")
+    if n.startswith("void "):
+        n = n[5:]
+    return n.split("(")[0]
+
+
+def main():
+    prof, tag, workload = sys.argv[1], sys.argv[2], sys.argv[3]
+    out = os.path.join(REPO, "profiles")
+    stats = glob.glob(os.path.join(prof, "trace", "*kernel_stats.csv"))
+    if stats:
+        shutil.copy(stats[0], os.path.join(out, f"{tag}_kernel_stats.csv"))
+    acc = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> values (one per dispatch)
+    for f in sorted(glob.glob(os.path.join(prof, "pmc*", "*counter_collection.csv"))):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                acc[short(row["Kernel_Name"])][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    rows = []
+    for k, counters in sorted(acc.items()):
+        for c, v in sorted(counters.items()):
+            rows.append([k, c, len(v), sum(v) / len(v), sum(v)])
+    with open(os.path.join(out, f"{tag}_pmc_summary.csv"), "w", newline="") as fh:
+        w = csv.writer(fh)
+        w.writerow(["kernel", "counter", "dispatches", "mean", "total"])
+        w.writerows(rows)
+    # the dominant kernel: all k_step instantiations of the run
+    fetch, write = [], []
+    for k, counters in acc.items():
+        if k.startswith("k_step"):
+            fetch += counters.get("FETCH_SIZE", [])
+            write += counters.get("WRITE_SIZE", [])
+    if fetch and write:
+        f_mean, w_mean = sum(fetch) / len(fetch), sum(write) / len(write)
+        traffic = {"kernel": "k_step", "workload": workload, "launches_fetch_pass": len(fetch),
+                   "launches_write_pass": len(write), "fetch_size_kib_mean": f_mean, "write_size_kib_mean": w_mean,
+                   "bytes_per_launch": (2.0 * f_mean + w_mean) * 1024.0,
+                   "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (KiB; gfx950 FETCH_SIZE counts half, "
+                              "MI355X_MICROARCH.md HBM [CDNA4])", "source": f"{tag}_pmc_summary.csv"}
+        with open(os.path.join(out, f"{tag}_traffic.json"), "w") as fh:
+            json.dump(traffic, fh, indent=1)
+        print(json.dumps(traffic))
+
+
+if __name__ == "__main__":
+    main()
