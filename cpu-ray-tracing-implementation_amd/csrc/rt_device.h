@@ -400,9 +400,24 @@ template <int K, class R>
 __device__ __forceinline__ R comp(V<R> v) {
   return K == 0 ? v.x : (K == 1 ? v.y : v.z);
 }
+// fp32 evaluates the test without branches: for non-negative floats the IEEE order is the
+// order of the bit patterns, so with 0 < tmin <= tmax
+//   tmin <= t <= tmax        <=>  bits(t) - bits(tmin) <= bits(tmax) - bits(tmin)  (unsigned)
+//   0 <= alpha, beta <= 1     <=>  max(bits(alpha), bits(beta)) <= bits(1.0f)
+// and NaN or negative values fail both (only alpha = -0.0, an exact edge hit, is decided
+// differently). One compare each instead of a branch per condition.
 template <int A, int U, int W, class R>
 __device__ __forceinline__ bool aquad_t(const R* f, V<R> o, V<R> d, V<R> inv, R tmin, R tmax, R& t) {
   R th = fdiv_inv(f[0] - comp<A>(o), comp<A>(d), comp<A>(inv));
+  if constexpr (sizeof(R) == 4) {
+    const R a = ((comp<U>(o) + th * comp<U>(d)) - f[1]) * f[3];
+    const R b = ((comp<W>(o) + th * comp<W>(d)) - f[2]) * f[4];
+    const uint32_t lo = __float_as_uint(tmin);
+    const bool in_t = __float_as_uint(th) - lo <= __float_as_uint(tmax) - lo;
+    const bool in_ab = max(__float_as_uint(a), __float_as_uint(b)) <= 0x3f800000u;
+    t = th;
+    return in_t & in_ab;
+  }
   if (!(tmin <= th && th <= tmax)) return false;
   R pu = (comp<U>(o) + th * comp<U>(d)) - f[1];
   R pv = (comp<W>(o) + th * comp<W>(d)) - f[2];
@@ -623,7 +638,10 @@ __device__ __forceinline__ void trace_linear(const DevScene<R>& sc, V<R> wo, V<R
     R th;
     bool h = false;
     if (ty == E_QUAD) {
-      if (!(op == excl_e && cur == excl_i)) h = lin_quad_t(rec, o, d, inv, tmin, tmax, th);
+      if constexpr (sizeof(R) == 4)  // evaluated for every lane, excluded lanes masked (no branch)
+        h = lin_quad_t(rec, o, d, inv, tmin, tmax, th) & !(op == excl_e && cur == excl_i);
+      else if (!(op == excl_e && cur == excl_i))
+        h = lin_quad_t(rec, o, d, inv, tmin, tmax, th);
     } else if (SPH && ty == E_SPHERE) {
       h = sphere_test(ld3(rec.f), ld3(rec.f + 4), rec.f[3], rec.aux != 0, o, d, time, tmin, tmax,
                       op == excl_e && cur == excl_i, th);
