@@ -80,6 +80,7 @@ struct Params {
   V<double> cdu, cdv, cdir00;  // the same in fp64: the fp32 path builds camera rays in fp64 and rounds once
   unsigned long long* seg_shards;
   int32_t K;  // segments per launch
+  Light<R> light;  // copy of the scene's light: kernel arguments are read with scalar loads
 };
 
 template <class R>
@@ -277,12 +278,12 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
     const Material<R>& m = sc.mats[mat];
     if (m.kind == M_DIFFUSE_LIGHT) {  // material.h:211-215; no scatter
       if (front) {
-        add = s.thr * tex_sample(sc.texs[m.tex], pw);
+        add = s.thr * tex_sample(m.tx, pw);
         has_add = true;
       }
       done = true;
     } else {
-      V<R> att = tex_sample(sc.texs[m.tex], pw);
+      V<R> att = tex_sample(m.tx, pw);
       const uint32_t bounce = (uint32_t)s.bounce;
       uint32_t js = 0;
       auto U = [&]() { return to_unit<R>(draw_u32(s.ks, dim_scatter(bounce, js++))); };
@@ -310,7 +311,7 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
         const R iso_pdf = R(1) / (R(4) * Num<R>::pi());
         Onb<R> b;
         if (!iso) b = make_onb(n);
-        const Light<R>& Lt = *sc.light;
+        const Light<R>& Lt = p.light;
         R pv;
         V<R> dir;
         if (Lt.kind == L_NONE) {  // camera.h:217-226
@@ -736,6 +737,7 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     unsigned char* sp = (unsigned char*)c->state.ptr;
     Params<R> p{};
     p.sc = dev_scene<R>(hdr, sbase);
+    std::memcpy(&p.light, (f64 ? cs.blob64 : cs.blob32).data() + hdr.off_light, sizeof(Light<R>));
     p.O = (R4<R>*)sp;
     p.D = (R4<R>*)(sp + r4);
     p.T = (R4<R>*)(sp + 2 * r4);

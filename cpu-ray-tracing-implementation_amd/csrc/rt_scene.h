@@ -146,19 +146,20 @@ enum : int32_t { M_LAMBERTIAN = 1, M_METAL = 2, M_DIELECTRIC = 3, M_ISOTROPIC = 
 enum : int32_t { T_SOLID = 1, T_CHECKER = 2 };
 
 template <class R>
-struct alignas(16) Material {
-  int32_t kind;
-  int32_t tex;
-  R fuzz;  // float in the reference (material.h:96); widened exactly
-  R refr;  // float in the reference (material.h:142)
-};
-
-template <class R>
 struct alignas(16) Texture {
   R c0[3];  // solid color / checker odd
   int32_t kind;
   R c1[3];  // checker even
   R scale;  // checker (texture.h:48)
+};
+// The material's texture is copied inline: shading reads one record per hit.
+template <class R>
+struct alignas(16) Material {
+  int32_t kind;
+  int32_t tex;
+  R fuzz;  // float in the reference (material.h:96); widened exactly
+  R refr;  // float in the reference (material.h:142)
+  Texture<R> tx;  // = texs[tex]
 };
 
 // The importance-sampling light (camera.h:135 `light`, hittable_list.h:39-50).

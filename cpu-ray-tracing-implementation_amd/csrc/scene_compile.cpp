@@ -657,7 +657,10 @@ Node<float> to32(const Node<double>& n) {
   r.child[1] = n.child[1];
   return r;
 }
-Material<float> to32(const Material<double>& m) { return {m.kind, m.tex, (float)m.fuzz, (float)m.refr}; }
+Texture<float> to32(const Texture<double>& t);
+Material<float> to32(const Material<double>& m) {
+  return {m.kind, m.tex, (float)m.fuzz, (float)m.refr, to32(m.tx)};
+}
 LinRec<float> to32(const LinRec<double>& l) {
   LinRec<float> r{};
   r.op = l.op;
@@ -818,7 +821,7 @@ bool Compiler::run(CompiledScene* out, std::string* err) {
       *err = "material kind " + std::to_string(m.kind) + " is not implemented on the device";
       return false;
     }
-    mats_.push_back({m.kind, m.texture, (double)m.fuzz, (double)m.refraction});
+    mats_.push_back({m.kind, m.texture, (double)m.fuzz, (double)m.refraction, texs_[m.texture]});
   }
   if (d_->background >= d_->num_textures) {
     *err = "background texture out of range";
