@@ -40,6 +40,9 @@ using namespace rtd;
 namespace {
 
 constexpr int kBlock = 256;
+#ifndef RT_LINEAR_WAVES
+#define RT_LINEAR_WAVES 6
+#endif
 constexpr int kBatch = 16;           // extend/shade rounds between live-slot counts
 constexpr int kSegShards = 256;      // segment counter shards
 constexpr uint32_t kAutoPool32 = 1u << 21;
@@ -383,6 +386,9 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
 template <class R, bool SPH, bool TRI, bool VOL>
 struct LinearTrav {
   static constexpr int kStack = 0;
+  // waves per SIMD the register budget is cut for (occupancy hides the shading loads); the
+  // lean quad-only program fits 96 VGPRs with a small spill, the others would spill heavily
+  static constexpr int kWaves = (sizeof(R) == 4 && !SPH && !TRI && !VOL) ? RT_LINEAR_WAVES : 1;
   __device__ __forceinline__ static void run(const DevScene<R>& sc, const Path<R>& s, Keys k, uint32_t*, R& t,
                                              uint32_t& e, int32_t& i) {
     trace_linear<R, SPH, TRI, VOL>(sc, s.o, s.d, s.tm, s.xe, s.xi, k, (uint32_t)s.bounce, t, e, i);
@@ -391,6 +397,7 @@ struct LinearTrav {
 template <class R, int STACK>
 struct StackTrav {
   static constexpr int kStack = STACK;
+  static constexpr int kWaves = 1;  // no constraint
   __device__ __forceinline__ static void run(const DevScene<R>& sc, const Path<R>& s, Keys k, uint32_t* stk, R& t,
                                              uint32_t& e, int32_t& i) {
     trace<R, STACK, kBlock>(sc, s.o, s.d, s.tm, s.xe, s.xi, k, (uint32_t)s.bounce, stk, t, e, i);
@@ -407,7 +414,7 @@ struct Lds<0> {
 };
 
 template <class R, class Trav>
-__global__ __launch_bounds__(kBlock) void k_step(Params<R> p) {
+__device__ __forceinline__ void step_body(const Params<R>& p) {
   __shared__ Lds<Trav::kStack * kBlock> stk;
   __shared__ uint32_t wave_cnt[kBlock / 64];
   uint32_t i = blockIdx.x * kBlock + threadIdx.x;
@@ -441,6 +448,17 @@ __global__ __launch_bounds__(kBlock) void k_step(Params<R> p) {
     uint32_t c = wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3];
     if (c) atomicAdd(&p.seg_shards[blockIdx.x % kSegShards], (unsigned long long)c);
   }
+}
+
+// The kernel; k_step_occ is the same body with the register budget cut for Trav::kWaves
+// waves per SIMD (only where that does not spill much, see LinearTrav::kWaves).
+template <class R, class Trav>
+__global__ __launch_bounds__(kBlock) void k_step(Params<R> p) {
+  step_body<R, Trav>(p);
+}
+template <class R, class Trav>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Trav::kWaves))) void k_step_occ(Params<R> p) {
+  step_body<R, Trav>(p);
 }
 
 // ------------------------------------------------------------------ live-slot compaction
@@ -657,7 +675,10 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
 
 template <class R, class Trav>
 void launch_k(const Params<R>& p, uint32_t grid, hipStream_t st) {
-  hipLaunchKernelGGL((k_step<R, Trav>), dim3(grid), dim3(kBlock), 0, st, p);
+  if constexpr (Trav::kWaves > 1)
+    hipLaunchKernelGGL((k_step_occ<R, Trav>), dim3(grid), dim3(kBlock), 0, st, p);
+  else
+    hipLaunchKernelGGL((k_step<R, Trav>), dim3(grid), dim3(kBlock), 0, st, p);
 }
 
 template <class R>
