@@ -31,6 +31,12 @@ $(BUILD)/librt_hip_trace.so: $(LIB_SRCS) $(LIB_HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DRT_DEBUG_TRACE -shared -o $@ $(LIB_SRCS)
 
+# development build with per-section shader clocks (scripts/dev_sections.py)
+sections: $(BUILD)/librt_hip_sections.so
+$(BUILD)/librt_hip_sections.so: $(LIB_SRCS) $(LIB_HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DRT_SECTION_CLOCKS -shared -o $@ $(LIB_SRCS)
+
 # the reference's config scenes written against the drop-in plugin surface (+ rtsc_* C ABI for tests)
 $(BUILD)/librt_scenes.so: $(PKG)/scenes/config_scenes.cpp $(PKG)/scenes/config_scenes.h $(RT_HDRS) $(BUILD)/librt_hip.so
 	$(CXX) $(CXXFLAGS) -shared -o $@ $(PKG)/scenes/config_scenes.cpp -L$(BUILD) -lrt_hip -Wl,-rpath,'$$ORIGIN'
@@ -46,4 +52,4 @@ clean:
 	rm -rf $(BUILD)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean precise trace
+.PHONY: all oracle clean precise trace sections

@@ -413,6 +413,10 @@ struct Lds<0> {
   uint32_t v[1];
 };
 
+#ifdef RT_SECTION_CLOCKS
+__device__ unsigned long long g_section_clocks[4];  // trace, shade, store, lanes
+#endif
+
 template <class R, class Trav>
 __device__ __forceinline__ void step_body(const Params<R>& p) {
   __shared__ Lds<Trav::kStack * kBlock> stk;
@@ -429,16 +433,41 @@ __device__ __forceinline__ void step_body(const Params<R>& p) {
   if (active) {
     Path<R> s;
     load_path(p, slot, Dv, s);
+#ifdef RT_SECTION_CLOCKS
+    uint64_t c_trace = 0, c_shade = 0;
+#endif
 #pragma unroll 1
     for (int k = 0; k < p.K; k++) {
       R t;
       uint32_t e;
       int32_t inst;
+#ifdef RT_SECTION_CLOCKS
+      const uint64_t c0 = clock64();
+#endif
       Trav::run(p.sc, s, Keys{s.ks}, stk.v + threadIdx.x, t, e, inst);
       segs++;
+#ifdef RT_SECTION_CLOCKS
+      const uint64_t c1 = clock64();
+      const bool more = shade(p, s, t, e, inst);
+      const uint64_t c2 = clock64();
+      c_trace += c1 - c0;
+      c_shade += c2 - c1;
+      if (!more) break;
+#else
       if (!shade(p, s, t, e, inst)) break;
+#endif
     }
+#ifdef RT_SECTION_CLOCKS
+    const uint64_t c3 = clock64();
+#endif
     store_path(p, slot, s);
+#ifdef RT_SECTION_CLOCKS
+    // development build: shader-clock cycles per section, summed over lanes (divide by the lane count)
+    atomicAdd(&g_section_clocks[0], (unsigned long long)c_trace);
+    atomicAdd(&g_section_clocks[1], (unsigned long long)c_shade);
+    atomicAdd(&g_section_clocks[2], (unsigned long long)(clock64() - c3));
+    atomicAdd(&g_section_clocks[3], 1ull);
+#endif
   }
   // segments traced: wave sums, one atomic per block
   for (int off = 32; off > 0; off >>= 1) segs += __shfl_xor(segs, off);
@@ -1017,6 +1046,15 @@ rt_status rt_set_timing(rt_context* c, int32_t enable) {
   c->timing = enable ? 1 : 0;
   return RT_OK;
 }
+
+#ifdef RT_SECTION_CLOCKS
+// development build only (scripts/dev_sections.py): read and clear the section clocks
+void rt_dev_section_clocks(unsigned long long out[4]) {
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(g_section_clocks), sizeof(unsigned long long) * 4);
+  unsigned long long z[4] = {0, 0, 0, 0};
+  hipMemcpyToSymbol(HIP_SYMBOL(g_section_clocks), z, sizeof(z));
+}
+#endif
 
 uint32_t rt_rng_u32(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t dim) {
   return draw_u32(key_path(key_pixel(seed, pixel), key_sample(seed, sample)), dim);
