@@ -706,8 +706,16 @@ template <class R>
 __device__ __forceinline__ Onb<R> make_onb(V<R> n) {
   Onb<R> b;
   b.y = unit(n);
-  V<R> a = (fabs(b.y.x) > R(0.9)) ? mkv(R(0), R(0), R(1)) : mkv(R(1), R(0), R(0));
-  b.z = unit(cross(b.y, a));
+  if constexpr (sizeof(R) == 4) {
+    // cross(y, a) for a = e_z or e_x has an exact zero component: (y.y, -y.x, 0) or (0, y.z, -y.y)
+    const bool ez = fabsf(b.y.x) > 0.9f;
+    const float c0 = ez ? b.y.y : 0.f, c1 = ez ? -b.y.x : b.y.z, c2 = ez ? 0.f : -b.y.y;
+    const float r = frsq(ez ? c0 * c0 + c1 * c1 : c1 * c1 + c2 * c2);
+    b.z = mkv(c0 * r, c1 * r, c2 * r);
+  } else {
+    V<R> a = (fabs(b.y.x) > R(0.9)) ? mkv(R(0), R(0), R(1)) : mkv(R(1), R(0), R(0));
+    b.z = unit(cross(b.y, a));
+  }
   b.x = cross(b.y, b.z);
   return b;
 }
@@ -738,11 +746,32 @@ __device__ __forceinline__ V<R> cosine_dir(R r1, R r2) {
 }
 
 // hittable_pdf over the light (hittable_list.h:39-50 -> quad.h:66-78 / sphere.h:76-81 / hittable.h:39-41)
+// `sampled`: dir came from light_random, i.e. dir = (a point on the light) - o. Then it hits the
+// light at t = 1 by construction, and fp32 uses that instead of re-testing: a point sampled on
+// the light's edge (u1 or u2 ~ 0) can round to just outside it, giving pdf 0 for a direction
+// the light itself produced (and 0/0 = NaN when the material pdf is 0 too).
 template <class R>
-__device__ __forceinline__ R light_pdf(const Light<R>& L, V<R> o, V<R> dir) {
+__device__ __forceinline__ R light_pdf(const Light<R>& L, V<R> o, V<R> dir, bool sampled = false) {
   if (L.kind == L_QUAD) {
     R t;
-    if (!quad_t(L.quad, o, dir, R(0.001), Num<R>::inf(), t)) return R(0);
+    bool hit;
+    if (sizeof(R) == 4 && sampled) {
+      t = R(1);
+      hit = true;
+    } else if (sizeof(R) == 4 && L.aligned) {  // uniform branch: the light is a kernel argument
+      const V<R> inv = rcp3(dir);
+      switch (L.aligned) {
+        case 1: hit = aquad_t<2, 0, 1>(L.af, o, dir, inv, R(0.001), Num<R>::inf(), t); break;
+        case 2: hit = aquad_t<1, 0, 2>(L.af, o, dir, inv, R(0.001), Num<R>::inf(), t); break;
+        case 3: hit = aquad_t<2, 1, 0>(L.af, o, dir, inv, R(0.001), Num<R>::inf(), t); break;
+        case 4: hit = aquad_t<0, 1, 2>(L.af, o, dir, inv, R(0.001), Num<R>::inf(), t); break;
+        case 5: hit = aquad_t<1, 2, 0>(L.af, o, dir, inv, R(0.001), Num<R>::inf(), t); break;
+        default: hit = aquad_t<0, 2, 1>(L.af, o, dir, inv, R(0.001), Num<R>::inf(), t); break;
+      }
+    } else {
+      hit = quad_t(L.quad, o, dir, R(0.001), Num<R>::inf(), t);
+    }
+    if (!hit) return R(0);
     R dist2 = t * t * dot(dir, dir);
     R cosine = fabs(dot(unit(dir), ld3(L.quad.n)));
     return fdiv(dist2, cosine * L.quad.area);

@@ -223,10 +223,12 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
     } else {
       V<R> oo = o, dd = d;
       const Instance<R>* in = nullptr;
-      if (inst >= 0) {
-        in = &sc.insts[inst];
-        chain_in(*in, oo, dd);
-      }
+      if (inst >= 0) in = &sc.insts[inst];
+      // fp32, planar primitives: instances are rigid, so the hit is o + t d in world space and
+      // only the object-space normal needs rotating out (fp64 keeps the reference's
+      // object-space point, hittable.h:75-82, 125-149)
+      const bool world_space = sizeof(R) == 4 && ty != E_SPHERE;
+      if (in && !world_space) chain_in(*in, oo, dd);
       V<R> po = oo + t * dd;
       V<R> outward;
       if (ty == E_QUAD) {
@@ -262,13 +264,21 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
         outward = ld3(tr.n);
         mat = tr.mat;
       }
-      front = dot(dd, outward) < R(0);  // hit_record::set_face_normal (hittable.h:26-29)
-      n = front ? outward : -outward;
-      pw = po;
-      if (in) {
-        for (int q = in->nops - 1; q >= 0; q--) {
-          pw = op_out(in->op[q], pw, true);
-          n = op_out(in->op[q], n, false);
+      if (world_space) {
+        if (in)
+          for (int q = in->nops - 1; q >= 0; q--) outward = op_out(in->op[q], outward, false);
+        front = dot(dd, outward) < R(0);  // hit_record::set_face_normal (hittable.h:26-29)
+        n = front ? outward : -outward;
+        pw = po;
+      } else {
+        front = dot(dd, outward) < R(0);  // hit_record::set_face_normal (hittable.h:26-29)
+        n = front ? outward : -outward;
+        pw = po;
+        if (in) {
+          for (int q = in->nops - 1; q >= 0; q--) {
+            pw = op_out(in->op[q], pw, true);
+            n = op_out(in->op[q], n, false);
+          }
         }
       }
     }
@@ -326,12 +336,13 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
           R c = U();
           R u1 = U();
           R u2 = U();
-          if (c < R(0.5))
+          const bool from_light = c < R(0.5);
+          if (from_light)
             dir = light_random(Lt, pw, u1, u2);
           else
             dir = iso ? unit(on_sphere(u1, u2)) : onb_transform(b, cosine_dir(u1, u2));
           R mp = iso ? iso_pdf : fmax(R(0), fdiv(dot(unit(dir), b.y), Num<R>::pi()));
-          pv = R(0.5) * light_pdf(Lt, pw, dir) + R(0.5) * mp;
+          pv = R(0.5) * light_pdf(Lt, pw, dir, from_light) + R(0.5) * mp;
         }
         R ps;
         if (iso) {
@@ -342,8 +353,8 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
         }
         if constexpr (sizeof(R) == 8)
           s.thr = s.thr * ((att * ps) / pv);  // camera.h:238 grouping on the parity path
-        else
-          s.thr = s.thr * (att * fdiv(ps, pv));
+        else  // a zero mixture pdf (the reference's 0/0 = NaN) ends the path
+          s.thr = pv > R(0) ? s.thr * (att * fdiv(ps, pv)) : mkv(R(0), R(0), R(0));
         new_d = dir;
       }
       new_o = pw;

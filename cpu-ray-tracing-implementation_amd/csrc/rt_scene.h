@@ -167,7 +167,8 @@ enum : int32_t { L_NONE = 0, L_BASE = 1, L_QUAD = 2, L_SPHERE = 3 };
 template <class R>
 struct alignas(16) Light {
   int32_t kind;
-  int32_t pad[3];
+  int32_t aligned;  // L_QUAD: 1 + perm when axis-aligned (af as a LinRec aligned quad), else 0
+  int32_t pad[2];
   Quad<R> quad;  // L_QUAD (quad.h:66-78)
   R u[3];
   R pad1;
@@ -175,6 +176,7 @@ struct alignas(16) Light {
   R pad2;
   R center[3];  // L_SPHERE: center_ (sphere.h:76-81)
   R radius;
+  R af[8];  // aligned L_QUAD: q[A], q[U], q[V], 1/u[U], 1/v[V], u[U], v[V]
 };
 
 // What the host uploads: offsets into one contiguous device blob.

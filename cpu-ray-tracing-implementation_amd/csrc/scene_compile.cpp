@@ -24,6 +24,8 @@
 
 namespace rtd {
 namespace {
+// perm -> (A, U, V): the plane axis and the axes of u and v (rt_scene.h LinRec)
+constexpr int kPermAxes[6][3] = {{2, 0, 1}, {1, 0, 2}, {2, 1, 0}, {0, 1, 2}, {1, 2, 0}, {0, 2, 1}};
 
 constexpr double kInf = std::numeric_limits<double>::infinity();
 constexpr int kSmallList = 8;  // lists up to this size stay ordered lists
@@ -565,6 +567,17 @@ void Compiler::light_from(int idx) {
     if (!ok_) return;
     light_.kind = L_QUAD;
     light_.quad = quads_.back();
+    if (aligned_.back()) {
+      const int* ax = kPermAxes[aligned_.back() - 1];
+      light_.aligned = aligned_.back();
+      light_.af[0] = light_.quad.q[ax[0]];
+      light_.af[1] = light_.quad.q[ax[1]];
+      light_.af[2] = light_.quad.q[ax[2]];
+      light_.af[3] = 1.0 / qu_.back();
+      light_.af[4] = 1.0 / qv_.back();
+      light_.af[5] = qu_.back();
+      light_.af[6] = qv_.back();
+    }
     quads_.resize(before);
     aligned_.resize(before);
     qu_.resize(before);
@@ -684,6 +697,8 @@ Light<float> to32(const Light<double>& l) {
   cvt3(r.v, l.v);
   cvt3(r.center, l.center);
   r.radius = (float)l.radius;
+  r.aligned = l.aligned;
+  for (int k = 0; k < 8; k++) r.af[k] = (float)l.af[k];
   return r;
 }
 template <class T>
@@ -728,7 +743,6 @@ SceneHeader pack(std::vector<unsigned char>& blob, const std::vector<Q>& q, cons
 }
 
 // perm -> (A, U, V): the plane axis and the axes of u and v (rt_scene.h LinRec)
-constexpr int kPermAxes[6][3] = {{2, 0, 1}, {1, 0, 2}, {2, 1, 0}, {0, 1, 2}, {1, 2, 0}, {0, 2, 1}};
 
 LinRec<double> Compiler::lin_record(uint32_t op) const {
   LinRec<double> r{};
