@@ -144,7 +144,9 @@ template <>
 struct Num<float> {
   static constexpr float inf() { return __builtin_huge_valf(); }
   static constexpr float pi() { return 3.14159265358979323846f; }
-  static constexpr float box_slack() { return 1.0f + 2.0f * 3.0f * 5.9604645e-08f; }  // 1 + 2*gamma(3)
+  // 1 + 2*gamma(5): the robust bound 1 + 2*gamma(3) for correctly rounded 1/d, widened for
+  // v_rcp_f32's 1-ulp reciprocal (box_inv)
+  static constexpr float box_slack() { return 1.0f + 2.0f * 5.0f * 5.9604645e-08f; }
 };
 template <>
 struct Num<double> {
@@ -211,7 +213,7 @@ struct DevScene {
   uint32_t root;
   int32_t background;
   int32_t has_volumes;
-  int32_t pad;
+  uint32_t n_nodes;
 };
 
 // World -> object through an instance chain (hittable.h:75-82, 125-135, 192-202, 259-270).
@@ -247,6 +249,15 @@ __device__ __forceinline__ void chain_in(const Instance<R>& in, V<R>& o, V<R>& d
 }
 
 // ------------------------------------------------------------------ primitive tests
+// 1/d for the slab test: v_rcp_f32 in fp32 (its error is covered by box_slack), IEEE in fp64.
+template <class R>
+__device__ __forceinline__ V<R> box_inv(V<R> d) {
+  if constexpr (sizeof(R) == 4)
+    return mkv(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
+  else
+    return mkv(R(1) / d.x, R(1) / d.y, R(1) / d.z);
+}
+
 // Ray/box slab test with IEEE min/max (a NaN slab is ignored: conservative) and
 // the robust 1 + 2*gamma(3) widening of the exit distance.
 template <class R>
@@ -508,22 +519,34 @@ __device__ bool volume_t(const DevScene<R>& sc, const Volume<R>& v, V<R> wo, V<R
 // world.hit(r, interval(0.001, inf), rec) (camera.h:198) as a stack machine.
 // excl_*: the surface the ray leaves (its previous hit); a planar primitive
 // cannot be re-hit from its own surface, a sphere only through its far side.
+#ifdef RT_SECTION_CLOCKS
+// development build: traversal counts (pops, node pops, primitive tests), summed over rays
+__device__ unsigned long long g_trace_totals[3];
+#define g_trace_counts tc
+#endif
 template <class R, int STACK, int BLOCK>
-__device__ void trace(const DevScene<R>& sc, V<R> wo, V<R> wd, R time, uint32_t excl_e, int32_t excl_i, Keys keys,
-                      uint32_t bounce, uint32_t* stk, R& t_best, uint32_t& e_best, int32_t& i_best) {
+__device__ void trace(const DevScene<R>& sc, const Node<R>* nodes, V<R> wo, V<R> wd, R time, uint32_t excl_e,
+                      int32_t excl_i, Keys keys, uint32_t bounce, uint32_t* stk, R& t_best, uint32_t& e_best,
+                      int32_t& i_best) {
   const R tmin = R(0.001);
   R tmax = Num<R>::inf();
   V<R> o = wo, d = wd;
-  V<R> inv = mkv(R(1) / d.x, R(1) / d.y, R(1) / d.z);
+  V<R> inv = box_inv(d);
   int32_t cur = -1;
   uint32_t jv = 0;
   int sp = 0;
+#ifdef RT_SECTION_CLOCKS
+  uint32_t tc[3] = {0, 0, 0};
+#endif
   e_best = kNoHit;
   i_best = -1;
   stk[0] = sc.root;
   sp = 1;
 
   auto test_prim = [&](uint32_t e) {
+#ifdef RT_SECTION_CLOCKS
+    g_trace_counts[2] += 1;
+#endif
     uint32_t ty = etype(e), i = epay(e);
     bool self = (e == excl_e) && (cur == excl_i);
     R th;
@@ -552,11 +575,22 @@ __device__ void trace(const DevScene<R>& sc, V<R> wo, V<R> wd, R time, uint32_t 
     }
   };
 
-  while (sp > 0) {
-    uint32_t e = stk[(--sp) * BLOCK];
-    uint32_t ty = etype(e);
-    if (ty == E_NODE) {
-      const Node<R>& nd = sc.nodes[epay(e)];
+  // "while-while" traversal (Aila & Laine 2009): each lane walks inner nodes until it holds a
+  // leaf entry (or its stack is empty), then the wave handles leaves together, so the box-test
+  // code and the primitive code are not both executed on every iteration of a divergent loop.
+  for (;;) {
+    uint32_t e = kEnd;
+    while (sp > 0) {
+      const uint32_t x = stk[(--sp) * BLOCK];
+#ifdef RT_SECTION_CLOCKS
+      g_trace_counts[0] += 1;  // pops (per lane; divided by segments on the host)
+      if (etype(x) == E_NODE) g_trace_counts[1] += 1;
+#endif
+      if (etype(x) != E_NODE) {
+        e = x;
+        break;
+      }
+      const Node<R>& nd = nodes[epay(x)];  // sc.nodes, or their copy in LDS
       R t0, t1;
       bool h0 = box_hit(nd.lo[0], nd.hi[0], o, inv, tmin, tmax, t0);
       bool h1 = box_hit(nd.lo[1], nd.hi[1], o, inv, tmin, tmax, t1);
@@ -574,7 +608,10 @@ __device__ void trace(const DevScene<R>& sc, V<R> wo, V<R> wd, R time, uint32_t 
       } else if (h1) {
         stk[(sp++) * BLOCK] = c1;
       }
-    } else if (ty == E_LIST) {
+    }
+    if (e == kEnd) break;
+    const uint32_t ty = etype(e);
+    if (ty == E_LIST) {
       uint32_t pos = epay(e);
       for (;;) {
         uint32_t r = sc.refs[pos];
@@ -601,7 +638,7 @@ __device__ void trace(const DevScene<R>& sc, V<R> wo, V<R> wd, R time, uint32_t 
       o = wo;
       d = wd;
       chain_in(in, o, d);
-      inv = mkv(R(1) / d.x, R(1) / d.y, R(1) / d.z);
+      inv = box_inv(d);
     } else if (ty == E_VOLUME) {
       test_volume(e);
     } else {  // RESTORE(k)
@@ -609,10 +646,15 @@ __device__ void trace(const DevScene<R>& sc, V<R> wo, V<R> wd, R time, uint32_t 
       o = wo;
       d = wd;
       if (cur >= 0) chain_in(sc.insts[cur], o, d);
-      inv = mkv(R(1) / d.x, R(1) / d.y, R(1) / d.z);
+      inv = box_inv(d);
     }
   }
   t_best = tmax;
+#ifdef RT_SECTION_CLOCKS
+  atomicAdd(&g_trace_totals[0], (unsigned long long)tc[0]);
+  atomicAdd(&g_trace_totals[1], (unsigned long long)tc[1]);
+  atomicAdd(&g_trace_totals[2], (unsigned long long)tc[2]);
+#endif
 }
 
 // Linear program (small scenes, rt_scene.h): every lane walks the same ops, so

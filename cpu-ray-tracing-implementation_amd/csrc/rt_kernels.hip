@@ -43,6 +43,9 @@ constexpr int kBlock = 256;
 #ifndef RT_LINEAR_WAVES
 #define RT_LINEAR_WAVES 6
 #endif
+#ifndef RT_STACK_WAVES
+#define RT_STACK_WAVES 3
+#endif
 constexpr int kBatch = 16;           // extend/shade rounds between live-slot counts
 constexpr int kSegShards = 256;      // segment counter shards
 constexpr uint32_t kAutoPool32 = 1u << 21;
@@ -400,18 +403,24 @@ struct LinearTrav {
   // waves per SIMD the register budget is cut for (occupancy hides the shading loads); the
   // lean quad-only program fits 96 VGPRs with a small spill, the others would spill heavily
   static constexpr int kWaves = (sizeof(R) == 4 && !SPH && !TRI && !VOL) ? RT_LINEAR_WAVES : 1;
-  __device__ __forceinline__ static void run(const DevScene<R>& sc, const Path<R>& s, Keys k, uint32_t*, R& t,
-                                             uint32_t& e, int32_t& i) {
+  static constexpr int kLdsNodes = 0;
+  __device__ __forceinline__ static void run(const DevScene<R>& sc, const Node<R>*, const Path<R>& s, Keys k,
+                                             uint32_t*, R& t, uint32_t& e, int32_t& i) {
     trace_linear<R, SPH, TRI, VOL>(sc, s.o, s.d, s.tm, s.xe, s.xi, k, (uint32_t)s.bounce, t, e, i);
   }
 };
-template <class R, int STACK>
+// LDSN: the scene's BVH nodes (at most kLdsNodeMax) are copied into LDS at kernel start, so
+// every traversal step reads LDS instead of waiting on the memory hierarchy (RTOW: 117 nodes)
+constexpr uint32_t kLdsNodeMax = 256;
+template <class R, int STACK, bool LDSN = false>
 struct StackTrav {
   static constexpr int kStack = STACK;
-  static constexpr int kWaves = 1;  // no constraint
-  __device__ __forceinline__ static void run(const DevScene<R>& sc, const Path<R>& s, Keys k, uint32_t* stk, R& t,
-                                             uint32_t& e, int32_t& i) {
-    trace<R, STACK, kBlock>(sc, s.o, s.d, s.tm, s.xe, s.xi, k, (uint32_t)s.bounce, stk, t, e, i);
+  static constexpr int kLdsNodes = LDSN ? (int)kLdsNodeMax : 0;
+  static constexpr int kWaves = sizeof(R) == 4 ? RT_STACK_WAVES : 1;  // fp32: occupancy over a small spill
+  __device__ __forceinline__ static void run(const DevScene<R>& sc, const Node<R>* nodes, const Path<R>& s, Keys k,
+                                             uint32_t* stk, R& t, uint32_t& e, int32_t& i) {
+    trace<R, STACK, kBlock>(sc, LDSN ? nodes : sc.nodes, s.o, s.d, s.tm, s.xe, s.xi, k, (uint32_t)s.bounce, stk,
+                            t, e, i);
   }
 };
 
@@ -432,6 +441,11 @@ template <class R, class Trav>
 __device__ __forceinline__ void step_body(const Params<R>& p) {
   __shared__ Lds<Trav::kStack * kBlock> stk;
   __shared__ uint32_t wave_cnt[kBlock / 64];
+  __shared__ Node<R> lds_nodes[Trav::kLdsNodes > 0 ? Trav::kLdsNodes : 1];
+  if constexpr (Trav::kLdsNodes > 0) {
+    for (uint32_t j = threadIdx.x; j < p.sc.n_nodes; j += kBlock) lds_nodes[j] = p.sc.nodes[j];
+    __syncthreads();
+  }
   uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   uint32_t slot = 0, segs = 0;
   bool active = i < p.n;
@@ -455,7 +469,7 @@ __device__ __forceinline__ void step_body(const Params<R>& p) {
 #ifdef RT_SECTION_CLOCKS
       const uint64_t c0 = clock64();
 #endif
-      Trav::run(p.sc, s, Keys{s.ks}, stk.v + threadIdx.x, t, e, inst);
+      Trav::run(p.sc, lds_nodes, s, Keys{s.ks}, stk.v + threadIdx.x, t, e, inst);
       segs++;
 #ifdef RT_SECTION_CLOCKS
       const uint64_t c1 = clock64();
@@ -710,6 +724,7 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
   s.root = h.root;
   s.background = h.background;
   s.has_volumes = h.has_volumes;
+  s.n_nodes = h.n_nodes;
   return s;
 }
 
@@ -733,6 +748,8 @@ void launch_step(const Params<R>& p, int stack, bool sph, bool tri, uint32_t gri
       launch_k<R, LinearTrav<R, true, false, false>>(p, grid, st);
     else
       launch_k<R, LinearTrav<R, true, true, true>>(p, grid, st);
+  } else if (sizeof(R) == 4 && p.sc.n_nodes <= kLdsNodeMax && stack <= 16) {
+    launch_k<R, StackTrav<R, 16, true>>(p, grid, st);
   } else if (stack <= 8) {
     launch_k<R, StackTrav<R, 8>>(p, grid, st);
   } else if (stack <= 16) {
@@ -1060,10 +1077,12 @@ rt_status rt_set_timing(rt_context* c, int32_t enable) {
 
 #ifdef RT_SECTION_CLOCKS
 // development build only (scripts/dev_sections.py): read and clear the section clocks
-void rt_dev_section_clocks(unsigned long long out[4]) {
+void rt_dev_section_clocks(unsigned long long out[7]) {
   hipMemcpyFromSymbol(out, HIP_SYMBOL(g_section_clocks), sizeof(unsigned long long) * 4);
+  hipMemcpyFromSymbol(out + 4, HIP_SYMBOL(rtd::g_trace_totals), sizeof(unsigned long long) * 3);
   unsigned long long z[4] = {0, 0, 0, 0};
   hipMemcpyToSymbol(HIP_SYMBOL(g_section_clocks), z, sizeof(z));
+  hipMemcpyToSymbol(HIP_SYMBOL(rtd::g_trace_totals), z, sizeof(unsigned long long) * 3);
 }
 #endif
 
