@@ -11,6 +11,11 @@
 
 namespace rtd {
 
+// fp32: spheres larger than this are intersected (and their hit points rebuilt) in fp64
+#ifndef RT_BIG_SPHERE_R
+#define RT_BIG_SPHERE_R 16
+#endif
+
 // Math policy. fp64 (the parity path): IEEE division/sqrt and libm, as the reference.
 // fp32 (the production path): the hardware ops -- v_rcp_f32, v_sqrt_f32, v_rsq_f32,
 // v_log_f32, and v_sin_f32 / v_cos_f32, which take their argument in revolutions, so
@@ -368,7 +373,7 @@ __device__ __forceinline__ bool sphere_test(V<R> c1, V<R> dc, R r, bool moving, 
     if (dot(d, o - c) >= R(0)) return false;  // leaving the sphere it starts on
     far_only = true;
   }
-  if (sizeof(R) == 4 && r > R(16)) {
+  if (sizeof(R) == 4 && r > R(RT_BIG_SPHERE_R)) {
     // big spheres (the RTOW ground, r = 1000): |o-c|^2 - r^2 cancels catastrophically in fp32
     double td;
     if (!sphere_roots<double>(o.x, o.y, o.z, d.x, d.y, d.z, c.x, c.y, c.z, r, tmin, tmax, far_only, td))

@@ -243,7 +243,7 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
         if constexpr (sizeof(R) == 8) {
           outward = (po - ld3(sp.cn)) / sp.r;
         } else {
-          if (sp.r > R(16)) {
+          if (sp.r > R(RT_BIG_SPHERE_R)) {
             // Big spheres (intersected in fp64, see sphere_test): o + t*d in fp32 is off the
             // surface by ~1e-7 absolute, enough to flip the sign of y near the top of the RTOW
             // ground (y = 0 under the glass sphere) and with it the checker parity
