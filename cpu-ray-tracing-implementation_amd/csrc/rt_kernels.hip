@@ -65,6 +65,24 @@ struct alignas(4 * sizeof(R)) R4 {
 //   A  running sum of the item     S  key_pixel, key of the running sample, item, sample
 //   X  the surface the ray leaves (entry, instance): self-intersection exclusion;
 //      the pixel (x | y << 16) and the end of the sample range of the slot's item
+// The camera as camera::render/generate_ray use it (camera.h:137-141, 244-290), in double.
+struct CamDev {
+  int32_t mode;  // rt_camera_mode
+  int32_t pad;
+  V<double> pos, du, dv;
+  V<double> dir00;   // perspective / fisheye: f dir - vw/2 right + vh/2 up + (du + dv)/2 (camera.h:246, 260)
+  V<double> pos00;   // orthonormal / lens: pos - vw/2 right + vh/2 up + (du + dv)/2 (camera.h:253, 278)
+  V<double> dir;     // dir_, unit
+  V<double> fdir;    // focus_dist_ * dir_ (camera.h:279)
+  V<double> disk_u, disk_v;  // defocus_disk_u/v (camera.h:129-131)
+  double focal;      // focal_length_ (camera.h:266)
+};
+
+// utility.h:46-52 random_in_unit_disk by rejection; attempt k draws dimensions kDimDisk + 2k
+// and + 2k + 1 (far above the per-bounce dimensions); the origin after kDiskTries failures
+// (probability (1 - pi/4)^64 ~ 1e-43). Same as the oracle.
+constexpr uint32_t kDimDisk = 0x7FFF0000u, kDiskTries = 64;
+
 template <class R>
 struct Params {
   DevScene<R> sc;
@@ -82,8 +100,11 @@ struct Params {
   uint32_t P, npix, n_items, chunk, spp, first_sample, W;
   int32_t max_depth;
   uint64_t seed;
-  V<R> pos, du, dv, dir00;
-  V<double> cdu, cdv, cdir00;  // the same in fp64: the fp32 path builds camera rays in fp64 and rounds once
+  // camera rays are built in fp64 for both paths (fp32 rounds once): the perspective camera
+  // from kernel arguments; the other models read the rest of CamDev (device memory, scalar loads)
+  V<double> cpos, cdu, cdv, cdir00;
+  int32_t cam_mode;
+  const CamDev* camx;
   unsigned long long* seg_shards;
   int32_t K;  // segments per launch
   Light<R> light;  // copy of the scene's light: kernel arguments are read with scalar loads
@@ -146,25 +167,70 @@ __device__ __forceinline__ void begin_item(const Params<R>& p, Path<R>& s, uint3
   s.ka = key_pixel(p.seed, gpix);
 }
 
+// camera::generate_ray for the orthonormal, fisheye and lens models (camera.h:252-290), reading
+// its fields from device memory. Only the CAMX kernel instantiations contain it, so the
+// perspective kernels' registers are not shaped by it.
+__device__ __forceinline__ void camera_ray(const CamDev* cp, uint32_t ks, uint32_t x, uint32_t y, double ox,
+                                        double oy, V<double>& o, V<double>& d, double& tm) {
+  const int32_t mode = ld_uniform(&cp->mode, 0);
+  const V<double> du = ld_uniform(&cp->du, 0), dv = ld_uniform(&cp->dv, 0);
+  o = ld_uniform(&cp->pos, 0);
+  if (mode == RT_CAM_ORTHONORMAL) {  // camera.h:252-258
+    const V<double> q = (ld_uniform(&cp->pos00, 0) + double(x) * du) + double(y) * dv;
+    o = (q + ox * du) + oy * dv;
+    d = ld_uniform(&cp->dir, 0);
+    tm = to_unit<double>(draw_u32(ks, 2));
+  } else if (mode == RT_CAM_LENS) {  // camera.h:276-283, 287-290
+    d = ((((ld_uniform(&cp->pos00, 0) + double(x) * du) + double(y) * dv) + ox * du) + oy * dv) +
+        ld_uniform(&cp->fdir, 0);
+    double px = 0, py = 0;
+    for (uint32_t k = 0; k < kDiskTries; k++) {
+      const double ax = -1 + 2 * to_unit<double>(draw_u32(ks, kDimDisk + 2 * k));
+      const double ay = -1 + 2 * to_unit<double>(draw_u32(ks, kDimDisk + 2 * k + 1));
+      if (ax * ax + ay * ay + 0.0 * 0.0 < 1) {
+        px = ax;
+        py = ay;
+        break;
+      }
+    }
+    o = o + (px * ld_uniform(&cp->disk_u, 0) + py * ld_uniform(&cp->disk_v, 0));
+    d = d - o;
+    tm = 0;  // ray(origin, direction): time 0, no draw
+  } else {  // fisheye (camera.h:259-275)
+    const V<double> dir = ld_uniform(&cp->dir, 0);
+    d = ((ld_uniform(&cp->dir00, 0) + double(x) * du) + double(y) * dv + ox * du) + oy * dv;
+    const V<double> w = d - dir;
+    const double r = sqrt(w.x * w.x + w.y * w.y + w.z * w.z);
+    const double theta = asin(r / ld_uniform(&cp->focal, 0));
+    const V<double> v1 = unit(dir), v2 = unit(d);
+    const double st = sin(theta);
+    const double b = sqrt(st * st / (1 - dot(v1, v2) * dot(v1, v2)));
+    const double a = cos(theta) - b * dot(v1, v2);
+    d = a * v1 + b * v2;
+    tm = to_unit<double>(draw_u32(ks, 2));
+  }
+}
+
 // camera::generate_ray, perspective mode (camera.h:244-251,293): sample s.sample of the slot's pixel
-template <class R>
+template <class R, bool CAMX>
 __device__ __forceinline__ void begin_sample(const Params<R>& p, Path<R>& s) {
   s.ks = key_path(s.ka, key_sample(p.seed, p.first_sample + s.sample));
   uint32_t x = s.xy & 0xFFFFu, y = s.xy >> 16;
-  R ox = to_unit<R>(draw_u32(s.ks, 0)) - R(0.5);  // exact in fp32 and fp64
-  R oy = to_unit<R>(draw_u32(s.ks, 1)) - R(0.5);
-  if constexpr (sizeof(R) == 4) {
-    // the correctly rounded fp64 direction: a few ulp less error on every camera ray, which
-    // otherwise shows up as paths that cross a checker line or sphere edge differently
-    V<double> rd = (p.cdir00 + double(x) * p.cdu) + double(y) * p.cdv;
-    V<double> dd = (rd + double(ox) * p.cdu) + double(oy) * p.cdv;
-    s.d = mkv(float(dd.x), float(dd.y), float(dd.z));
-  } else {
-    V<R> rd = (p.dir00 + R(x) * p.du) + R(y) * p.dv;
-    s.d = (rd + ox * p.du) + oy * p.dv;
+  // In fp64 for both paths: fp32 gets the correctly rounded ray, a few ulp less error on every
+  // camera ray, which otherwise shows up as paths crossing a checker line or edge differently.
+  const double ox = to_unit<double>(draw_u32(s.ks, 0)) - 0.5;  // sample_square (camera.h:293)
+  const double oy = to_unit<double>(draw_u32(s.ks, 1)) - 0.5;
+  V<double> o = p.cpos, d;
+  double tm;
+  if (!CAMX || p.cam_mode == RT_CAM_PERSPECTIVE) {  // camera.h:245-251
+    d = ((p.cdir00 + double(x) * p.cdu) + double(y) * p.cdv + ox * p.cdu) + oy * p.cdv;
+    tm = to_unit<double>(draw_u32(s.ks, 2));
+  } else if constexpr (CAMX) {
+    camera_ray(p.camx, s.ks, x, y, ox, oy, o, d, tm);
   }
-  s.tm = to_unit<R>(draw_u32(s.ks, 2));
-  s.o = p.pos;
+  s.o = mkv(R(o.x), R(o.y), R(o.z));
+  s.d = mkv(R(d.x), R(d.y), R(d.z));
+  s.tm = R(tm);
   s.bounce = 0;
   s.thr = mkv(R(1), R(1), R(1));
   s.rad = mkv(R(0), R(0), R(0));
@@ -172,7 +238,8 @@ __device__ __forceinline__ void begin_sample(const Params<R>& p, Path<R>& s) {
   s.xi = -1;
 }
 
-template <class R>
+
+template <class R, bool CAMX>
 __global__ __launch_bounds__(kBlock) void k_init(Params<R> p) {
   uint32_t slot = blockIdx.x * kBlock + threadIdx.x;
   if (slot >= p.P) return;
@@ -183,7 +250,7 @@ __global__ __launch_bounds__(kBlock) void k_init(Params<R> p) {
     s.bounce = -1;
   } else {
     begin_item(p, s, slot);
-    begin_sample(p, s);
+    begin_sample<R, CAMX>(p, s);
   }
   store_path(p, slot, s);
 }
@@ -192,7 +259,7 @@ __global__ __launch_bounds__(kBlock) void k_init(Params<R> p) {
 // closest hit (t, e, inst) of s's ray, add emission, scatter (or finish the
 // sample and regenerate the slot's next camera ray). Returns false once the slot
 // has no work left.
-template <class R>
+template <class R, bool CAMX>
 __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t inst) {
   const DevScene<R>& sc = p.sc;
   V<R> add = mkv(R(0), R(0), R(0));
@@ -322,7 +389,18 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
         else
           new_d = refract(ud, n, ri);
         s.thr = s.thr * att;
-      } else {  // lambertian (material.h:62-72) / isotropic (material.h:193-200): kRandom
+      } else if (m.kind == M_GLOSS && to_unit<R>(draw_u32(s.ks, dim_scatter(bounce, js))) <= m.spec) {
+        // gloss, specular branch (material.h:158-167): kDetermined, attenuation 1,
+        // direction unit(lerp(smoothness, cosine-hemisphere sample about n, reflect(d_in, n)))
+        js++;
+        const Onb<R> b = make_onb(n);
+        const R r1 = U();
+        const R r2 = U();
+        const V<R> diffuse = onb_transform(b, cosine_dir(r1, r2));
+        const R tt = m.smooth;
+        new_d = unit((R(1) - tt) * diffuse + tt * reflect(d, n));
+      } else {  // lambertian (material.h:62-72) / isotropic (material.h:193-200) / gloss diffuse: kRandom
+        if (m.kind == M_GLOSS) js++;  // the specular-choice draw above (material.h:161)
         const bool iso = m.kind == M_ISOTROPIC;
         const R iso_pdf = R(1) / (R(4) * Num<R>::pi());
         Onb<R> b;
@@ -389,7 +467,7 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
     }
     begin_item(p, s, s.item + p.P);
   }
-  begin_sample(p, s);
+  begin_sample<R, CAMX>(p, s);
   return true;
 }
 
@@ -437,7 +515,7 @@ struct Lds<0> {
 __device__ unsigned long long g_section_clocks[4];  // trace, shade, store, lanes
 #endif
 
-template <class R, class Trav>
+template <class R, class Trav, bool CAMX>
 __device__ __forceinline__ void step_body(const Params<R>& p) {
   __shared__ Lds<Trav::kStack * kBlock> stk;
   __shared__ uint32_t wave_cnt[kBlock / 64];
@@ -473,13 +551,13 @@ __device__ __forceinline__ void step_body(const Params<R>& p) {
       segs++;
 #ifdef RT_SECTION_CLOCKS
       const uint64_t c1 = clock64();
-      const bool more = shade(p, s, t, e, inst);
+      const bool more = shade<R, CAMX>(p, s, t, e, inst);
       const uint64_t c2 = clock64();
       c_trace += c1 - c0;
       c_shade += c2 - c1;
       if (!more) break;
 #else
-      if (!shade(p, s, t, e, inst)) break;
+      if (!shade<R, CAMX>(p, s, t, e, inst)) break;
 #endif
     }
 #ifdef RT_SECTION_CLOCKS
@@ -506,13 +584,14 @@ __device__ __forceinline__ void step_body(const Params<R>& p) {
 
 // The kernel; k_step_occ is the same body with the register budget cut for Trav::kWaves
 // waves per SIMD (only where that does not spill much, see LinearTrav::kWaves).
-template <class R, class Trav>
+// CAMX: the camera is not perspective (camera_ray); the perspective kernels do not contain it.
+template <class R, class Trav, bool CAMX>
 __global__ __launch_bounds__(kBlock) void k_step(Params<R> p) {
-  step_body<R, Trav>(p);
+  step_body<R, Trav, CAMX>(p);
 }
-template <class R, class Trav>
+template <class R, class Trav, bool CAMX>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Trav::kWaves))) void k_step_occ(Params<R> p) {
-  step_body<R, Trav>(p);
+  step_body<R, Trav, CAMX>(p);
 }
 
 // ------------------------------------------------------------------ live-slot compaction
@@ -604,24 +683,33 @@ __global__ void k_zero(R* out, uint64_t n) {
   if (i < n) out[i] = R(0);
 }
 
-// camera.h:137-141 and 246 evaluated in double exactly as the reference orders them
-struct View {
-  double du[3], dv[3], dir00[3], pos[3];
-};
-View make_view(const rt_camera_desc* c) {
-  View v;
+// camera.h:137-141, 246, 253, 278-279 evaluated in double exactly as the reference orders them
+CamDev make_view(const rt_camera_desc* c) {
+  CamDev v{};
+  v.mode = c->mode;
+  double du[3], dv[3], dir00[3], pos00[3];
   for (int k = 0; k < 3; k++) {
-    v.du[k] = (c->right[k] * c->viewport_width) / (double)c->image_width;
-    v.dv[k] = (c->up[k] * -c->viewport_height) / (double)c->image_height;
+    du[k] = (c->right[k] * c->viewport_width) / (double)c->image_width;
+    dv[k] = (c->up[k] * -c->viewport_height) / (double)c->image_height;
   }
   for (int k = 0; k < 3; k++) {
     double a = c->dir[k] * c->focal_length;
     double b = c->right[k] * (c->viewport_width / 2.0);
     double u = c->up[k] * (c->viewport_height / 2.0);
-    double e = (v.du[k] + v.dv[k]) * 0.5;
-    v.dir00[k] = ((a - b) + u) + e;
-    v.pos[k] = c->pos[k];
+    double e = (du[k] + dv[k]) * 0.5;
+    dir00[k] = ((a - b) + u) + e;
+    pos00[k] = ((c->pos[k] - b) + u) + e;
   }
+  v.pos = {c->pos[0], c->pos[1], c->pos[2]};
+  v.du = {du[0], du[1], du[2]};
+  v.dv = {dv[0], dv[1], dv[2]};
+  v.dir00 = {dir00[0], dir00[1], dir00[2]};
+  v.pos00 = {pos00[0], pos00[1], pos00[2]};
+  v.dir = {c->dir[0], c->dir[1], c->dir[2]};
+  v.fdir = {c->focus_dist * c->dir[0], c->focus_dist * c->dir[1], c->focus_dist * c->dir[2]};
+  v.disk_u = {c->defocus_u[0], c->defocus_u[1], c->defocus_u[2]};
+  v.disk_v = {c->defocus_v[0], c->defocus_v[1], c->defocus_v[2]};
+  v.focal = c->focal_length;
   return v;
 }
 
@@ -646,7 +734,8 @@ struct rt_context {
   CompiledScene scene;
   bool has_scene = false;
   DevBuf scene32, scene64;
-  DevBuf state, partial, pixmap, queue0, queue1, blk, out_tmp, counters;
+  DevBuf state, partial, pixmap, queue0, queue1, blk, out_tmp, counters, camx;
+  CamDev cam_host;  // source of camx (kept alive for the async copy)
   uint32_t* total_host = nullptr;  // pinned
   uint64_t samples = 0;
   rt_counters last{};
@@ -730,10 +819,18 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
 
 template <class R, class Trav>
 void launch_k(const Params<R>& p, uint32_t grid, hipStream_t st) {
-  if constexpr (Trav::kWaves > 1)
-    hipLaunchKernelGGL((k_step_occ<R, Trav>), dim3(grid), dim3(kBlock), 0, st, p);
-  else
-    hipLaunchKernelGGL((k_step<R, Trav>), dim3(grid), dim3(kBlock), 0, st, p);
+  const bool camx = p.cam_mode != RT_CAM_PERSPECTIVE;
+  if constexpr (Trav::kWaves > 1) {
+    if (camx)
+      hipLaunchKernelGGL((k_step_occ<R, Trav, true>), dim3(grid), dim3(kBlock), 0, st, p);
+    else
+      hipLaunchKernelGGL((k_step_occ<R, Trav, false>), dim3(grid), dim3(kBlock), 0, st, p);
+  } else {
+    if (camx)
+      hipLaunchKernelGGL((k_step<R, Trav, true>), dim3(grid), dim3(kBlock), 0, st, p);
+    else
+      hipLaunchKernelGGL((k_step<R, Trav, false>), dim3(grid), dim3(kBlock), 0, st, p);
+  }
 }
 
 template <class R>
@@ -836,19 +933,23 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     p.W = (uint32_t)cam->image_width;
     p.max_depth = prm->max_depth;
     p.seed = prm->seed;
-    View vw = make_view(cam);
-    p.pos = tov<R>(vw.pos);
-    p.du = tov<R>(vw.du);
-    p.dv = tov<R>(vw.dv);
-    p.dir00 = tov<R>(vw.dir00);
-    p.cdu = tov<double>(vw.du);
-    p.cdv = tov<double>(vw.dv);
-    p.cdir00 = tov<double>(vw.dir00);
+    c->cam_host = make_view(cam);
+    if ((s = ensure(c, c->camx, sizeof(CamDev))) != RT_OK) return s;
+    RT_HIP(c, hipMemcpyAsync(c->camx.ptr, &c->cam_host, sizeof(CamDev), hipMemcpyHostToDevice, st));
+    p.cpos = c->cam_host.pos;
+    p.cdu = c->cam_host.du;
+    p.cdv = c->cam_host.dv;
+    p.cdir00 = c->cam_host.dir00;
+    p.cam_mode = c->cam_host.mode;
+    p.camx = (const CamDev*)c->camx.ptr;
     p.seg_shards = (unsigned long long*)c->counters.ptr;
     const int K = prm->segments_per_launch > 0 ? std::min(prm->segments_per_launch, 64) : kAutoSegments;
     p.K = K;
 
-    hipLaunchKernelGGL(k_init<R>, dim3(nblk_max), dim3(kBlock), 0, st, p);
+    if (p.cam_mode != RT_CAM_PERSPECTIVE)
+      hipLaunchKernelGGL((k_init<R, true>), dim3(nblk_max), dim3(kBlock), 0, st, p);
+    else
+      hipLaunchKernelGGL((k_init<R, false>), dim3(nblk_max), dim3(kBlock), 0, st, p);
     uint64_t launches = 1, iters = 0;
     uint32_t* qbuf[2] = {(uint32_t*)c->queue0.ptr, (uint32_t*)c->queue1.ptr};
     int qsel = 0;
@@ -974,7 +1075,7 @@ void rt_context_destroy(rt_context* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->scene32, &c->scene64, &c->state, &c->partial, &c->pixmap, &c->queue0, &c->queue1, &c->blk,
-                    &c->out_tmp, &c->counters})
+                    &c->out_tmp, &c->counters, &c->camx})
     if (b->ptr) (void)hipFree(b->ptr);
   for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
   if (c->total_host) (void)hipHostFree(c->total_host);
@@ -1033,8 +1134,8 @@ rt_status rt_render_tiles(rt_context* c, const rt_camera_desc* cam, const rt_ren
   if (!cam || !prm || (!tiles && ntiles > 0) || ntiles < 0 || (!out_rgb && ntiles > 0))
     return set_err(c, RT_ERR_INVALID_ARGUMENT, "null argument");
   if (!c->has_scene) return set_err(c, RT_ERR_NO_SCENE, "rt_scene_upload has not succeeded on this context");
-  if (cam->mode != RT_CAM_PERSPECTIVE)
-    return set_err(c, RT_ERR_UNSUPPORTED, "only the perspective camera (camera.h:245-251) runs on the device");
+  if (cam->mode < RT_CAM_PERSPECTIVE || cam->mode > RT_CAM_LENS)
+    return set_err(c, RT_ERR_INVALID_ARGUMENT, "unknown camera mode");
   if (cam->image_width <= 0 || cam->image_height <= 0) return set_err(c, RT_ERR_INVALID_ARGUMENT, "empty image");
   if (prm->spp <= 0) return set_err(c, RT_ERR_INVALID_ARGUMENT, "spp must be positive");
   if (prm->precision != RT_PREC_F32 && prm->precision != RT_PREC_F64)

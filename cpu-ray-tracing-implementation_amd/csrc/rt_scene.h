@@ -142,7 +142,7 @@ struct alignas(16) Node {
   uint32_t child[2];
 };
 
-enum : int32_t { M_LAMBERTIAN = 1, M_METAL = 2, M_DIELECTRIC = 3, M_ISOTROPIC = 4, M_DIFFUSE_LIGHT = 5 };
+enum : int32_t { M_LAMBERTIAN = 1, M_METAL = 2, M_DIELECTRIC = 3, M_ISOTROPIC = 4, M_DIFFUSE_LIGHT = 5, M_GLOSS = 6 };
 enum : int32_t { T_SOLID = 1, T_CHECKER = 2 };
 
 template <class R>
@@ -159,6 +159,8 @@ struct alignas(16) Material {
   int32_t tex;
   R fuzz;  // float in the reference (material.h:96); widened exactly
   R refr;  // float in the reference (material.h:142)
+  R smooth, spec;  // gloss: smoothness_ clamped to [0, 1] and specular_prob_ (material.h:147-155)
+  R pad[2];
   Texture<R> tx;  // = texs[tex]
 };
 

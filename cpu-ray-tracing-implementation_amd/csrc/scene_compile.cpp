@@ -672,7 +672,7 @@ Node<float> to32(const Node<double>& n) {
 }
 Texture<float> to32(const Texture<double>& t);
 Material<float> to32(const Material<double>& m) {
-  return {m.kind, m.tex, (float)m.fuzz, (float)m.refr, to32(m.tx)};
+  return {m.kind, m.tex, (float)m.fuzz, (float)m.refr, (float)m.smooth, (float)m.spec, {0, 0}, to32(m.tx)};
 }
 LinRec<float> to32(const LinRec<double>& l) {
   LinRec<float> r{};
@@ -831,11 +831,14 @@ bool Compiler::run(CompiledScene* out, std::string* err) {
       *err = "material " + std::to_string(i) + " has no valid texture";
       return false;
     }
-    if (m.kind < RT_MAT_LAMBERTIAN || m.kind > RT_MAT_DIFFUSE_LIGHT) {
+    if (m.kind < RT_MAT_LAMBERTIAN || m.kind > RT_MAT_GLOSS) {
       *err = "material kind " + std::to_string(m.kind) + " is not implemented on the device";
       return false;
     }
-    mats_.push_back({m.kind, m.texture, (double)m.fuzz, (double)m.refraction, texs_[m.texture]});
+    // gloss: interval(0, 1).clamp(smoothness) (material.h:149, interval.h) -- NaN passes through
+    const float sm = m.smoothness < 0.f ? 0.f : (m.smoothness > 1.f ? 1.f : m.smoothness);
+    mats_.push_back({m.kind, m.texture, (double)m.fuzz, (double)m.refraction, (double)sm, (double)m.specular_prob,
+                     {0, 0}, texs_[m.texture]});
   }
   if (d_->background >= d_->num_textures) {
     *err = "background texture out of range";

@@ -31,8 +31,9 @@ class SceneBuilder:
         return len(self.textures) - 1
 
     # materials (material.h)
-    def _mat(self, kind, tex, fuzz=0.0, refraction=1.0):
-        self.materials.append(abi.rt_material(kind=kind, texture=tex, fuzz=fuzz, refraction=refraction))
+    def _mat(self, kind, tex, fuzz=0.0, refraction=1.0, smoothness=0.0, specular_prob=0.0):
+        self.materials.append(abi.rt_material(kind=kind, texture=tex, fuzz=fuzz, refraction=refraction,
+                                              smoothness=smoothness, specular_prob=specular_prob))
         return len(self.materials) - 1
 
     def lambertian(self, tex):
@@ -49,6 +50,9 @@ class SceneBuilder:
 
     def diffuse_light(self, tex):
         return self._mat(abi.RT_MAT_DIFFUSE_LIGHT, tex)
+
+    def gloss(self, tex, smoothness, specular_prob):  # material.h:145-155 (smoothness clamped on compile)
+        return self._mat(abi.RT_MAT_GLOSS, tex, smoothness=smoothness, specular_prob=specular_prob)
 
     # hittables
     def _obj(self, **kw):
@@ -141,3 +145,49 @@ def perspective(image_width, aspect, pos, lookat, focal_length=1.0, fovy_degree=
                            viewport_width=vw, viewport_height=vh, focal_length=focal, focus_dist=3.4)
     c.pos[:], c.dir[:], c.right[:], c.up[:] = list(pos), list(d), list(right), list(up)
     return c
+
+
+def _frame(pos, lookat):
+    """camera.h:23-28: dir, right, up from pos and lookat with world up (0, 1, 0)."""
+    pos, lookat = np.asarray(pos, float), np.asarray(lookat, float)
+    unit = lambda v: v / math.sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2])
+    cross = lambda a, b: np.array([a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]])
+    d = unit(lookat - pos)
+    right = unit(cross(d, np.array([0.0, 1.0, 0.0])))
+    return pos, d, right, cross(right, d)
+
+
+def _desc(mode, image_width, h, pos, d, right, up, vw, vh, focal=1.0, focus=3.4, du=(0, 0, 0), dv=(0, 0, 0)):
+    c = abi.rt_camera_desc(mode=mode, image_width=image_width, image_height=h, viewport_width=vw,
+                           viewport_height=vh, focal_length=focal, focus_dist=focus)
+    c.pos[:], c.dir[:], c.right[:], c.up[:] = list(pos), list(d), list(right), list(up)
+    c.defocus_u[:], c.defocus_v[:] = list(du), list(dv)
+    return c
+
+
+def orthonormal(image_width, aspect, viewport_height, pos, lookat):
+    """camera::initialize_orthnormal (camera.h:52-72)."""
+    pos, d, right, up = _frame(pos, lookat)
+    h = max(1, int(image_width / aspect))
+    return _desc(abi.RT_CAM_ORTHONORMAL, image_width, h, pos, d, right, up,
+                 viewport_height * (float(image_width) / h), viewport_height)
+
+
+def fisheye(image_width, aspect, pos, lookat, focal_length=1.0, fovy_degree=90.0):
+    """camera::initialize_fisheye (camera.h:74-100): the perspective frame, fisheye ray mapping."""
+    c = perspective(image_width, aspect, pos, lookat, focal_length, fovy_degree)
+    c.mode = abi.RT_CAM_FISHEYE
+    return c
+
+
+def lens(image_width, aspect, pos, lookat, defocus_angle, focus_dist=1.0, fovy_degree=90.0):
+    """camera::initialize_lens (camera.h:102-132): float aspect ratio, float angles and focus distance."""
+    pos, d, right, up = _frame(pos, lookat)
+    f32 = np.float32
+    h = max(1, int(f32(image_width) / f32(aspect)))  # int / float is a float division
+    focus = float(f32(focus_dist))
+    theta = float(f32(float(f32(fovy_degree)) * math.pi / 180.0))
+    vh = 2.0 * math.tan(theta / 2.0) * focus
+    vw = vh * (float(image_width) / h)
+    r = focus * math.tan(float(f32(defocus_angle) / f32(2)) * math.pi / 180.0)
+    return _desc(abi.RT_CAM_LENS, image_width, h, pos, d, right, up, vw, vh, 1.0, focus, right * r, up * r)

@@ -7,7 +7,7 @@ reference's main() implicitly does.
 import ctypes
 import math
 
-from .scene import SceneBuilder, perspective
+from .scene import SceneBuilder, fisheye, lens, orthonormal, perspective
 
 _libc = ctypes.CDLL(None)
 _libc.rand.restype = ctypes.c_int
@@ -134,6 +134,33 @@ def three_material_ball(width=1280, aspect=16.0 / 9.0):  # main.cc:67-84
     return s.desc(world, background=s.solid((0.7, 0.8, 1.0))), cam, 100, 5
 
 
+def three_material_ball_with_defocus_blur(width=1280, aspect=16.0 / 9.0):  # main.cc:87-103
+    desc, _, spp, depth = three_material_ball(width, aspect)
+    cam = lens(width, aspect, (13, 2, 3), (1, 1, 1), 2.0, 15, 20.0)
+    return desc, cam, 1000, 5
+
+
+def cornell_glossy(width=600, aspect=1.0):
+    """Cornell box with four gloss spheres of rising specular probability, the materials of
+    cornell_box_with_glossy_ball (main.cc:309-343) with solid colours instead of the earth image."""
+    s = SceneBuilder()
+    red, white = s.lambertian(s.solid((.65, .05, .05))), s.lambertian(s.solid((.73, .73, .73)))
+    green, light = s.lambertian(s.solid((.12, .45, .15))), s.diffuse_light(s.solid((15, 15, 15)))
+    walls = [s.quad((555, 0, 0), (0, 555, 0), (0, 0, 555), green), s.quad((0, 0, 0), (0, 555, 0), (0, 0, 555), red),
+             s.quad((0, 0, 0), (555, 0, 0), (0, 0, 555), white),
+             s.quad((555, 555, 555), (-555, 0, 0), (0, 0, -555), white),
+             s.quad((0, 0, 555), (555, 0, 0), (0, 555, 0), white)]
+    lq = s.quad((343, 554, 332), (-130, 0, 0), (0, 0, -105), light)
+    tex = s.solid((0.2, 0.4, 0.8))
+    balls = [s.sphere((110 + 110 * k, 90, 250), 80, s.gloss(tex, sm, sp))
+             for k, (sm, sp) in enumerate([(1.0, 1.0), (1.0, 0.4), (0.6, 0.15), (1.5, 0.02)])]
+    world = s.hlist(walls + balls + [lq])
+    cam = perspective(width, aspect, (278, 278, -800), (278, 278, 0), 1, 40.0)
+    return s.desc(world, light=lq), cam, 100, 8
+
+
 SCENES = {"cornell_box": cornell_box, "cornell_triangles": cornell_triangles, "cornell_box_with_volume": cornell_box_with_volume,
           "rtow": rtow, "rtow_motion": lambda **kw: rtow(moving=True, **kw),
-          "three_material_ball": three_material_ball}
+          "three_material_ball": three_material_ball,
+          "three_material_ball_with_defocus_blur": three_material_ball_with_defocus_blur,
+          "cornell_glossy": cornell_glossy}

@@ -38,7 +38,6 @@ class camera {
     viewport_height_ = 2.0 * std::tan(theta / 2.0) * focal_length_;
     viewport_width_ = viewport_height_ * (double(image_width_) / image_height_);
   }
-  // The other camera models keep the reference's parameters; the device renders perspective only so far.
   void initialize_orthnormal(int image_width, double aspect_ratio, double viewport_height, point3 pos, vec3 lookat,
                              int sample_per_pixel = 100, int max_recur_depth = 5) {
     mode_ = kOrthnormal;
@@ -57,6 +56,10 @@ class camera {
                        int max_recur_depth = 5) {
     mode_ = kLens;
     frame(image_width, aspect_ratio, pos, lookat, sample_per_pixel, max_recur_depth);
+    // camera.h:114: aspect_ratio is a float parameter here, so int / float divides in float
+    image_height_ = int(image_width / aspect_ratio);
+    image_height_ = image_height_ < 1 ? 1 : image_height_;
+    image_.assign((size_t)image_width_ * image_height_, color(0));
     fovy_degree_ = fovy_degree;
     focus_dist_ = focus_dist;
     float theta = (float)degrees_to_radians(fovy_degree_);
@@ -86,7 +89,6 @@ class camera {
   // Renders into image_ without writing a file. Returns false (reason in last_error_) on failure.
   bool render_image(const hittable& world, const std::shared_ptr<const hittable>& light = nullptr) {
     last_error_.clear();
-    if (mode_ != kPerspective) return fail("only the perspective camera runs on the device so far");
     scene_builder sb;
     int w, l = -1, bg = -1;
     try {

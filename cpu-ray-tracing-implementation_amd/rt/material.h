@@ -71,7 +71,7 @@ class dielectric : public material {  // material.h:100-143
   float refract_;
 };
 
-class gloss : public material {  // material.h:145-185 (CPU oracle only for now: the device rejects it)
+class gloss : public material {  // material.h:145-185
  public:
   gloss(std::shared_ptr<texture> albedo, float smoothness, float specular_prob) : tex_(std::move(albedo)) {
     smoothness_ = (float)interval(0, 1).clamp(smoothness);

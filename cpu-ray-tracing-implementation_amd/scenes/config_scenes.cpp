@@ -121,6 +121,23 @@ void three_material_ball(int width, double aspect, config_scene* s) {  // main.c
   s->cam.background_ = std::make_shared<solid_color>(color(0.7, 0.8, 1.0));
 }
 
+void three_material_ball_with_defocus_blur(int width, double aspect, config_scene* s) {  // main.cc:87-103
+  auto world = std::make_shared<hittable_list>();
+  auto ground = std::make_shared<lambertian>(
+      std::make_shared<checker_texture>(color{1.0, 1.0, 1.0}, color{0.6, 0.6, 0.2}, 1.0));
+  auto glass = std::make_shared<dielectric>(std::make_shared<solid_color>(color{1.0, 1.0, 1.0}), 1.5);
+  auto matte = std::make_shared<lambertian>(std::make_shared<solid_color>(color(0.4, 0.2, 0.1)));
+  auto metal_mat = std::make_shared<metal>(std::make_shared<solid_color>(color(0.7, 0.6, 0.5)), 0.0);
+  world->push_back(std::make_shared<sphere>(point3(0, -1000, 0), 1000, ground));
+  world->push_back(std::make_shared<sphere>(point3(0, 1, 0), 1.0, glass));
+  world->push_back(std::make_shared<sphere>(point3(-4, 1, 0), 1.0, matte));
+  world->push_back(std::make_shared<sphere>(point3(4, 1, 0), 1.0, metal_mat));
+  s->world = world;
+  s->cam.initialize_lens(W(width, 1280), (float)A(aspect, 16.0 / 9.0), point3(13, 2, 3), vec3(1, 1, 1), 2.0, 15,
+                         20.0, 1000, 5);
+  s->cam.background_ = std::make_shared<solid_color>(color(0.7, 0.8, 1.0));
+}
+
 }  // namespace
 
 bool build_config_scene(const std::string& name, int width, double aspect, config_scene* out) {
@@ -132,6 +149,8 @@ bool build_config_scene(const std::string& name, int width, double aspect, confi
     random_motion_ball(width, aspect, name == "rtow_motion", out);
   else if (name == "three_material_ball")
     three_material_ball(width, aspect, out);
+  else if (name == "three_material_ball_with_defocus_blur")
+    three_material_ball_with_defocus_blur(width, aspect, out);
   else
     return false;
   return true;

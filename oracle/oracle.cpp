@@ -791,31 +791,91 @@ struct integrator {
   }
 };
 
-struct view {  // precomputed per render (camera.h:137-141, 246)
+struct view {  // precomputed per render (camera.h:137-141, 246, 253, 260, 278)
+  int mode = RT_CAM_PERSPECTIVE;
   v3 du, dv, dir00, pos;
+  v3 pos00;          // orthonormal / lens: pos - vw/2 right + vh/2 up + (du + dv)/2 (camera.h:253, 278)
+  v3 dir, fdir;      // dir_ (unit) and focus_dist_ * dir_ (camera.h:279)
+  double focal = 1;  // focal_length_ (camera.h:266)
+  v3 disk_u, disk_v; // defocus_disk_u/v (camera.h:129-131)
 };
 
 inline view make_view(const rt_camera_desc& c) {
   view v;
   v3 right = v3_from(c.right), up = v3_from(c.up), dir = v3_from(c.dir);
+  v.mode = c.mode;
   v.du = c.viewport_width * right / c.image_width;
   v.dv = -c.viewport_height * up / c.image_height;
   v.dir00 = c.focal_length * dir - c.viewport_width / 2.0 * right + c.viewport_height / 2.0 * up + 0.5 * (v.du + v.dv);
   v.pos = v3_from(c.pos);
+  v.pos00 = v.pos - c.viewport_width / 2.0 * right + c.viewport_height / 2.0 * up + 0.5 * (v.du + v.dv);
+  v.dir = dir;
+  v.fdir = c.focus_dist * dir;
+  v.focal = c.focal_length;
+  v.disk_u = v3_from(c.defocus_u);
+  v.disk_v = v3_from(c.defocus_v);
   return v;
 }
 
-inline ray3 generate_ray(const view& vw, int y, int x, rngctx& g) {  // camera.h:244-251,293
-  v3 ray_dir = vw.dir00 + x * vw.du + y * vw.dv;
-  double ox, oy;
+// camera.h:293 sample_square: (U - 1/2, U - 1/2); GCC evaluates vec3(...) arguments right to left
+inline void sample_square(rngctx& g, double& ox, double& oy) {
   if (g.mode == ORC_RNG_COMPAT) {
-    oy = g.camera(1) - 0.5;  // GCC evaluates vec3(...) arguments right to left
+    oy = g.camera(1) - 0.5;
     ox = g.camera(0) - 0.5;
   } else {
     ox = g.camera(0) - 0.5;
     oy = g.camera(1) - 0.5;
   }
+}
+
+// utility.h:46-52 random_in_unit_disk by rejection. Counter mode: attempt k draws dimensions
+// kDimDisk + 2k (x) and + 2k + 1 (y); both modes give up after kDiskTries (never reached in
+// practice: (1 - pi/4)^64 ~ 1e-43) and return the origin.
+enum : uint32_t { kDimDisk = 0x7FFF0000u, kDiskTries = 64 };
+inline void random_in_unit_disk(rngctx& g, double& px, double& py) {
+  for (uint32_t k = 0; k < kDiskTries; k++) {
+    if (g.mode == ORC_RNG_COMPAT) {
+      py = -1 + 2 * g.glibc();  // random_double(-1, 1) (utility.h:22), right-to-left
+      px = -1 + 2 * g.glibc();
+    } else {
+      px = -1 + 2 * g.at(kDimDisk + 2 * k);
+      py = -1 + 2 * g.at(kDimDisk + 2 * k + 1);
+    }
+    if (px * px + py * py + 0.0 * 0.0 < 1) return;  // length_squared of (x, y, 0)
+  }
+  px = py = 0;
+}
+
+inline ray3 generate_ray(const view& vw, int y, int x, rngctx& g) {  // camera.h:244-284
+  double ox, oy;
+  if (vw.mode == RT_CAM_ORTHONORMAL) {  // camera.h:252-258
+    v3 p = vw.pos00 + x * vw.du + y * vw.dv;
+    sample_square(g, ox, oy);
+    v3 rp = p + ox * vw.du + oy * vw.dv;
+    double tm = g.camera(2);
+    return {rp, vw.dir, tm};
+  }
+  if (vw.mode == RT_CAM_LENS) {  // camera.h:276-283, 287-290
+    sample_square(g, ox, oy);
+    v3 rd = vw.pos00 + x * vw.du + y * vw.dv + ox * vw.du + oy * vw.dv + vw.fdir;
+    double px, py;
+    random_in_unit_disk(g, px, py);
+    v3 org = vw.pos + (px * vw.disk_u + py * vw.disk_v);
+    rd = rd - org;
+    return {org, rd, 0.0};  // ray(origin, direction): time 0, no draw
+  }
+  v3 ray_dir = vw.dir00 + x * vw.du + y * vw.dv;
+  sample_square(g, ox, oy);
   v3 d = ray_dir + ox * vw.du + oy * vw.dv;
+  if (vw.mode == RT_CAM_FISHEYE) {  // camera.h:259-275
+    double r = len(d - vw.dir);  // vec3::length (vec3.h:31-32)
+    double theta = std::asin(r / vw.focal);
+    v3 v1 = unit(vw.dir);
+    v3 v2 = unit(d);
+    double b = std::sqrt(std::sin(theta) * std::sin(theta) / (1 - dot(v1, v2) * dot(v1, v2)));
+    double a = std::cos(theta) - b * dot(v1, v2);
+    d = a * v1 + b * v2;
+  }
   double tm = g.camera(2);
   return {vw.pos, d, tm};
 }
@@ -1126,7 +1186,7 @@ void* orc_scene_from_desc(const rt_scene_desc* d, char* err, int errlen) {
     mm->tex = b.tex[m.texture];
     mm->fuzz = m.fuzz;
     mm->refr = m.refraction;
-    mm->smooth = m.smoothness;
+    mm->smooth = m.smoothness < 0.f ? 0.f : (m.smoothness > 1.f ? 1.f : m.smoothness);  // material.h:149
     mm->spec = m.specular_prob;
     s->mats.push_back(std::move(mm));
     b.mat.push_back(s->mats.back().get());
@@ -1187,7 +1247,9 @@ void orc_scene_free(void* p) { delete static_cast<scene*>(p); }
 int orc_render(const void* scp, const rt_camera_desc* cam, int spp, int first_sample, int max_depth,
                uint64_t seed, int rng_mode, int threads, const rt_tile* tiles, int ntiles, double* out,
                uint64_t* segments) {
-  if (!scp || !cam || !tiles || ntiles <= 0 || !out || spp <= 0 || cam->mode != RT_CAM_PERSPECTIVE) return 1;
+  if (!scp || !cam || !tiles || ntiles <= 0 || !out || spp <= 0 || cam->mode < RT_CAM_PERSPECTIVE ||
+      cam->mode > RT_CAM_LENS)
+    return 1;
   job jb;
   jb.sc = static_cast<const scene*>(scp);
   jb.vw = make_view(*cam);

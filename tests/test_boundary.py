@@ -75,9 +75,14 @@ def test_scene_check_volume_list_keeps_reference_order():
 
 def test_unsupported_material_is_rejected():
     s = SceneBuilder()
-    m = s._mat(abi.RT_MAT_GLOSS, s.solid((1, 1, 1)))
+    m = s._mat(9, s.solid((1, 1, 1)))  # not a material.h kind
     st, _, msg = abi.scene_check(s.desc(s.sphere((0, 0, 0), 1, m)))
     assert st == abi.RT_ERR_UNSUPPORTED and "material kind" in msg
+    # gloss (material.h:145-185) compiles for the device
+    s2 = SceneBuilder()
+    g = s2.gloss(s2.solid((1, 1, 1)), 0.5, 0.3)
+    st, _, msg = abi.scene_check(s2.desc(s2.sphere((0, 0, 0), 1, g)))
+    assert st == abi.RT_OK, msg
 
 
 def test_bad_descriptors_are_rejected():

@@ -172,6 +172,50 @@ def test_bvh_stack_traversal_matches_oracle(ctx):
     assert bad.any(-1).mean() < 1e-3, np.abs(img - ref).max()
 
 
+def _camera_variants():
+    from rt_amd.scene import fisheye, lens, orthonormal
+    return {
+        "orthonormal": orthonormal(40, 1.0, 555.0, (278, 278, -800), (278, 278, 0)),  # camera.h:52-72, 252-258
+        "fisheye": fisheye(40, 1.0, (278, 278, -600), (278, 278, 0), 1, 110.0),  # camera.h:74-100, 259-275
+        "lens": lens(40, 1.0, (278, 278, -800), (278, 278, 0), 3.0, 1000.0, 40.0),  # camera.h:102-132, 276-290
+    }
+
+
+@pytest.mark.parametrize("mode", ["orthonormal", "fisheye", "lens"])
+@pytest.mark.parametrize("precision", [F32, F64])
+def test_camera_modes_match_oracle(ctx, mode, precision):
+    desc, _, _, _ = scenes.cornell_box(width=40)
+    cam = _camera_variants()[mode]
+    img, ref, _ = render_both(ctx, desc, cam, 8, 6, 4, precision)
+    assert np.isfinite(ref).all() and np.isfinite(img).all()
+    if precision == F64:
+        assert np.all(np.abs(img - ref) <= 1e-9 * np.maximum(1.0, np.abs(ref))), np.abs(img - ref).max()
+    else:
+        assert (rmse(img, ref) < 1e-4).all(), rmse(img, ref)
+
+
+def test_defocus_blur_config_scene(ctx):
+    # main.cc:87-103 through the C++ plugin surface (initialize_lens): fp64 == oracle
+    cs = plugin.ConfigScene("three_material_ball_with_defocus_blur", 48)
+    img, ref, _ = render_both(ctx, cs.desc, cs.cam, 8, 5, 2, F64)
+    assert np.all(np.abs(img - ref) <= 1e-9 * np.maximum(1.0, np.abs(ref))), np.abs(img - ref).max()
+    img32, _, _ = render_both(ctx, cs.desc, cs.cam, 8, 5, 2, F32)
+    np.testing.assert_allclose(img32.reshape(-1, 3).mean(0), ref.reshape(-1, 3).mean(0), rtol=5e-3)
+
+
+@pytest.mark.parametrize("precision", [F32, F64])
+def test_gloss_matches_oracle(ctx, precision):
+    # material.h:145-185: specular branch (kDetermined lerp of cosine sample and reflection) and
+    # diffuse branch (kRandom, mixture with the light); smoothness 1.5 is clamped to 1
+    desc, cam, _, _ = scenes.cornell_glossy(width=40)
+    img, ref, _ = render_both(ctx, desc, cam, 8, 8, 6, precision)
+    if precision == F64:
+        assert np.all(np.abs(img - ref) <= 1e-9 * np.maximum(1.0, np.abs(ref))), np.abs(img - ref).max()
+    else:
+        assert np.mean(np.abs(img - ref).max(-1) > 1e-3) < 0.01
+        assert (rmse(img, ref) < 2e-3).all(), rmse(img, ref)
+
+
 def test_full_c2_fp32_matches_fp64(ctx):
     # BASELINE config 2 at full size: the fp32 production path against the fp64 device path
     cs = plugin.ConfigScene("cornell_box", 800)
@@ -207,12 +251,12 @@ def test_edge_cases(ctx):
     with pytest.raises(abi.RTError) as e:
         ctx.render(cam, 1, 1, tiles=[(20, 20, 8, 8)])
     assert e.value.status == abi.RT_ERR_INVALID_ARGUMENT
-    # a camera model the device does not run yet
+    # an unknown camera model
     bad = perspective(8, 1.0, (0, 0, -5), (0, 0, 0))
-    bad.mode = abi.RT_CAM_LENS
+    bad.mode = 7
     with pytest.raises(abi.RTError) as e:
         ctx.render(bad, 1, 1)
-    assert e.value.status == abi.RT_ERR_UNSUPPORTED
+    assert e.value.status == abi.RT_ERR_INVALID_ARGUMENT
 
 
 def test_errors_before_upload_and_unsupported_scene():
@@ -222,7 +266,7 @@ def test_errors_before_upload_and_unsupported_scene():
         c.render(cam, 1, 1)
     assert e.value.status == abi.RT_ERR_NO_SCENE
     s = SceneBuilder()
-    m = s._mat(abi.RT_MAT_GLOSS, s.solid((1, 1, 1)))
+    m = s._mat(9, s.solid((1, 1, 1)))  # no such material
     with pytest.raises(abi.RTError) as e:
         c.upload(s.desc(s.sphere((0, 0, 0), 1, m)))
     assert e.value.status == abi.RT_ERR_UNSUPPORTED

@@ -11,6 +11,7 @@ import oracle
 from rt_amd import abi, plugin, scenes
 
 NAMES = ["cornell_box", "cornell_box_with_volume", "rtow", "rtow_motion", "three_material_ball"]
+PY_NAMES = NAMES + ["three_material_ball_with_defocus_blur"]
 
 
 @pytest.mark.parametrize("name", NAMES)
@@ -24,7 +25,7 @@ def test_plugin_scene_matches_oracle_restatement(name):
     assert np.array_equal(a, b) and sa == sb
 
 
-@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("name", PY_NAMES)
 def test_python_builder_matches_plugin(name):
     cs = plugin.ConfigScene(name, 24)
     desc, cam, _, _ = scenes.SCENES[name](width=24)
