@@ -87,7 +87,7 @@ typedef enum rt_material_kind {
   RT_MAT_DIELECTRIC = 3,    /* material.h:100-143 refraction (float, material.h:142)    */
   RT_MAT_ISOTROPIC = 4,     /* material.h:187-204 */
   RT_MAT_DIFFUSE_LIGHT = 5, /* material.h:206-219 */
-  RT_MAT_GLOSS = 6          /* material.h:145-185 (not yet on the device: RT_ERR_UNSUPPORTED) */
+  RT_MAT_GLOSS = 6          /* material.h:145-185  smoothness (clamped to [0,1]), specular_prob */
 } rt_material_kind;
 
 typedef struct rt_material {
@@ -132,9 +132,9 @@ typedef struct rt_scene_desc {
 
 typedef enum rt_camera_mode {
   RT_CAM_PERSPECTIVE = 0, /* camera.h:245-251 */
-  RT_CAM_ORTHONORMAL = 1, /* camera.h:252-258 (not yet on the device) */
-  RT_CAM_FISHEYE = 2,     /* camera.h:259-275 (not yet on the device) */
-  RT_CAM_LENS = 3         /* camera.h:276-283 (not yet on the device) */
+  RT_CAM_ORTHONORMAL = 1, /* camera.h:252-258 */
+  RT_CAM_FISHEYE = 2,     /* camera.h:259-275 */
+  RT_CAM_LENS = 3         /* camera.h:276-290 (defocus disk by rejection sampling) */
 } rt_camera_mode;
 
 typedef struct rt_camera_desc {
