@@ -37,8 +37,22 @@ CONFIGS = {
     "c1": ("cornell_box", 400, 1.0, 64, 8),
     "c2": ("cornell_box", 800, 1.0, 1024, 50),
     "c3": ("rtow", 1200, 1.5, 512, 50),
+    "c4": ("sponza", 1920, 16.0 / 9.0, 256, 5),
     "c5": ("cornell_box_with_volume", 3840, 16.0 / 9.0, 4096, 5),
 }
+
+
+def sponza_asset():
+    """C4's glTF: $RT_SPONZA_GLTF (the real Sponza, if supplied), else the synthetic stand-in
+    (rt_amd.synth_gltf: 262,267 triangles, same camera and light) written to a temp directory."""
+    path = os.environ.get("RT_SPONZA_GLTF")
+    if path and os.path.exists(path):
+        return path, "Sponza glTF " + path
+    import tempfile
+    from rt_amd import synth_gltf
+    path = synth_gltf.write_sponza_standin(tempfile.mkdtemp(prefix="sponza_standin_"))
+    os.environ["RT_SPONZA_GLTF"] = path
+    return path, "synthetic Sponza stand-in (rt_amd.synth_gltf, 262,267 triangles; Sponza.bin is not shipped)"
 
 
 def cpu_baseline(scene_name, width, aspect, spp, depth, seed, threads):
@@ -108,6 +122,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     scene_name, width, aspect, spp, depth = CONFIGS[args.config]
+    asset = sponza_asset()[1] if scene_name == "sponza" else None
     # the scene exactly as the drop-in camera::render flattens it (C++ plugin surface, main.cc:198-225)
     cs = plugin.ConfigScene(scene_name, width, aspect)
     cam = cs.cam
@@ -202,7 +217,7 @@ def main():
             "value": round(value, 2), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "fp32" if prec == abi.RT_PREC_F32 else "fp64",
-            "data": "synthetic (the reference's Cornell Box scene, procedurally built; no assets)",
+            "data": asset or "synthetic (the reference's scene, procedurally built; no assets)",
             "config": {"workload": f"{scene_name} {W}x{H} {spp}spp depth {depth}, light sampling on",
                        "key": workload_key(scene_name, W, H, spp, depth, args),
                        "image": [W, H], "spp": spp, "max_depth": depth, "tiles": "64x64 round-robin over ranks",

@@ -16,6 +16,8 @@
 #include "scene_compile.h"
 
 #include <algorithm>
+#include <string>
+#include <unordered_map>
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -150,6 +152,9 @@ class Compiler {
   std::vector<Node<double>> nodes_;
   std::vector<uint32_t> refs_;
   std::vector<Material<double>> mats_;
+  std::vector<int32_t> mat_remap_;                    // descriptor material -> mats_ index
+  std::unordered_map<std::string, int32_t> mat_index_;  // material record bytes -> mats_ index
+  int32_t mat_id(int32_t m) const { return mat_remap_[(size_t)m]; }
   std::vector<Texture<double>> texs_;
   Light<double> light_{};
   int depth_guard_ = 0;
@@ -206,7 +211,7 @@ Item Compiler::prim_item(const rt_object& o) {
     double w[3] = {n[0] / nn, n[1] / nn, n[2] / nn};
     v_cross(o.c, w, q.a);  // alpha = dot(w, cross(p, v)) = dot(p, cross(v, w))
     v_cross(w, o.b, q.b);  // beta  = dot(w, cross(u, p)) = dot(p, cross(w, u))
-    q.mat = o.material;
+    q.mat = mat_id(o.material);
     quads_.push_back(q);
     it.entry = mk(E_QUAD, (uint32_t)quads_.size() - 1);
     // axis-aligned: u and v each along one axis, on different axes (then n is exactly +-e_A)
@@ -247,7 +252,7 @@ Item Compiler::prim_item(const rt_object& o) {
       s.cn[k] = o.moving ? 0.0 : o.a[k];
     }
     s.r = r;
-    s.mat = o.material;
+    s.mat = mat_id(o.material);
     s.moving = o.moving ? 1 : 0;
     spheres_.push_back(s);
     it.entry = mk(E_SPHERE, (uint32_t)spheres_.size() - 1);
@@ -274,7 +279,7 @@ Item Compiler::prim_item(const rt_object& o) {
     double n[3];
     v_cross(t.e1, t.e2, n);
     v_unit(n, t.n);
-    t.mat = o.material;
+    t.mat = mat_id(o.material);
     tris_.push_back(t);
     it.entry = mk(E_TRI, (uint32_t)tris_.size() - 1);
     it.box.grow(o.a);
@@ -534,7 +539,7 @@ void Compiler::gather(int idx, const std::vector<Op>& chain, std::vector<Item>& 
       v.neg_inv_density = -1.0 / o->s0;
       v.inst = chain2.empty() ? -1 : make_instance(chain2, bl.entry);
       v.boundary = bl.entry;
-      v.phase_mat = o->material;
+      v.phase_mat = mat_id(o->material);
       vols_.push_back(v);
       Item it{};
       it.entry = mk(E_VOLUME, (uint32_t)vols_.size() - 1);
@@ -837,8 +842,27 @@ bool Compiler::run(CompiledScene* out, std::string* err) {
     }
     // gloss: interval(0, 1).clamp(smoothness) (material.h:149, interval.h) -- NaN passes through
     const float sm = m.smoothness < 0.f ? 0.f : (m.smoothness > 1.f ? 1.f : m.smoothness);
-    mats_.push_back({m.kind, m.texture, (double)m.fuzz, (double)m.refraction, (double)sm, (double)m.specular_prob,
-                     {0, 0}, texs_[m.texture]});
+    Material<double> r{m.kind, m.texture, (double)m.fuzz, (double)m.refraction, (double)sm,
+                       (double)m.specular_prob, {0, 0}, texs_[m.texture]};
+    // value-identical materials share one record (main.cc:476-484 gives each of Sponza's
+    // 262k triangles its own lambertian(solid_color(1))): the key is everything shading reads
+    std::string key;
+    auto put = [&key](const void* p, size_t n) { key.append((const char*)p, n); };
+    put(&r.kind, 4);
+    put(&r.fuzz, 8);
+    put(&r.refr, 8);
+    put(&r.smooth, 8);
+    put(&r.spec, 8);
+    put(&r.tx.kind, 4);
+    put(r.tx.c0, 24);
+    put(r.tx.c1, 24);
+    put(&r.tx.scale, 8);
+    auto it = mat_index_.find(key);
+    if (it == mat_index_.end()) {
+      it = mat_index_.emplace(key, (int32_t)mats_.size()).first;
+      mats_.push_back(r);
+    }
+    mat_remap_.push_back(it->second);
   }
   if (d_->background >= d_->num_textures) {
     *err = "background texture out of range";

@@ -21,6 +21,9 @@ def load():
         L.rtsc_build.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_double, P(abi.rt_scene_desc),
                                  P(abi.rt_camera_desc), P(ctypes.c_int), P(ctypes.c_int), ctypes.c_char_p, ctypes.c_int]
         L.rtsc_free.argtypes = [ctypes.c_void_p]
+        L.rtsc_gltf_triangles.restype = ctypes.c_longlong
+        L.rtsc_gltf_triangles.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_char_p,
+                                          ctypes.c_int]
         L.rtsc_render_ppm.restype = ctypes.c_int
         L.rtsc_render_ppm.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_uint64, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
@@ -55,3 +58,17 @@ def render_ppm(name, path, width=0, aspect=0.0, spp=0, max_depth=0, seed=1, prec
     rc = load().rtsc_render_ppm(name.encode(), width, aspect, spp, max_depth, seed, precision, path.encode(), err, 512)
     if rc != 0:
         raise RuntimeError(f"camera::render failed: {err.value.decode()}")
+
+
+def gltf_triangles(path):
+    """The triangles main.cc's sponza() builds from a glTF file (gltf_loader.h quirks included),
+    as an (n, 3, 3) float64 array."""
+    import numpy as np
+    L = load()
+    err = ctypes.create_string_buffer(512)
+    n = L.rtsc_gltf_triangles(path.encode(), None, 0, err, 512)
+    if n < 0:
+        raise RuntimeError(f"glTF load failed: {err.value.decode()}")
+    out = np.zeros((max(n, 1), 3, 3), dtype=np.float64)
+    L.rtsc_gltf_triangles(path.encode(), out.ctypes.data, n, err, 512)
+    return out[:n]

@@ -3,9 +3,12 @@
 // descriptor camera::render would hand to librt_hip.
 #include "config_scenes.h"
 
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <vector>
+
+#include "../rt/gltf_loader.h"
 
 namespace {
 
@@ -138,6 +141,61 @@ void three_material_ball_with_defocus_blur(int width, double aspect, config_scen
   s->cam.background_ = std::make_shared<solid_color>(color(0.7, 0.8, 1.0));
 }
 
+// main.cc:447-485: the triangles sponza() builds from the loader's output primitives -- float
+// positions only, uint16 indices only (other index types leave the primitive empty), and
+// consecutive position triples when a primitive has no indices.
+std::vector<std::array<vec3, 3>> gltf_triangles(std::vector<OutputPrimitives>& prims) {
+  std::vector<std::array<vec3, 3>> out;
+  for (auto& pr : prims) {
+    std::vector<vec3> pos;
+    std::vector<unsigned short> idx;
+    if (pr.pos_type == DataType::kFloat) {
+      for (size_t j = 0; j + 12 <= pr.positions.size(); j += 3 * sizeof(float)) {
+        float x, y, z;
+        std::memcpy(&x, &pr.positions[j], 4);
+        std::memcpy(&y, &pr.positions[j + 4], 4);
+        std::memcpy(&z, &pr.positions[j + 8], 4);
+        pos.push_back(vec3(x, y, z));
+      }
+    }
+    if (pr.use_indices && pr.indices_type == DataType::kUnsignedShort) {
+      for (size_t j = 0; j + 2 <= pr.indices.size(); j += sizeof(unsigned short)) {
+        unsigned short k;
+        std::memcpy(&k, &pr.indices[j], 2);
+        idx.push_back(k);
+      }
+    }
+    auto at = [&](size_t k) -> const vec3& {
+      if (k >= pos.size()) throw std::runtime_error("glTF: index past the positions");
+      return pos[k];
+    };
+    if (pr.use_indices) {
+      for (size_t i = 0; i + 2 < idx.size(); i += 3) out.push_back({at(idx[i]), at(idx[i + 1]), at(idx[i + 2])});
+    } else {
+      for (size_t i = 0; i + 2 < pos.size(); i += 3) out.push_back({pos[i], pos[i + 1], pos[i + 2]});
+    }
+  }
+  return out;
+}
+
+// main.cc:439-498. The asset path is $RT_SPONZA_GLTF, else the reference's relative path.
+void sponza(int width, double aspect, config_scene* s) {
+  const char* env = std::getenv("RT_SPONZA_GLTF");
+  gltf::GltfLoader model(env && *env ? env : "./assets/Sponza/glTF/Sponza.gltf");
+  auto& prims = model.getOutputPrimitives();
+  hittable_list world;
+  for (const auto& t : gltf_triangles(prims))
+    world.push_back(std::make_shared<triangle>(t[0], t[1], t[2],
+                                               std::make_shared<lambertian>(std::make_shared<solid_color>(color(1.0f)))));
+  auto light = std::make_shared<diffuse_light>(color(10));
+  auto quad_light = std::make_shared<quad>(point3(0, 1200, 0), vec3(500, 0, 0), vec3(0, 0, 500), light);
+  world.push_back(quad_light);
+  s->world = std::make_shared<bvh_node>(world);
+  s->light = quad_light;
+  s->cam.initialize_perspective(W(width, 200), A(aspect, 1.0), point3(500, 320, 90), point3(0, 280, 0), 1, 45.0, 30,
+                                5);
+}
+
 }  // namespace
 
 bool build_config_scene(const std::string& name, int width, double aspect, config_scene* out) {
@@ -151,6 +209,8 @@ bool build_config_scene(const std::string& name, int width, double aspect, confi
     three_material_ball(width, aspect, out);
   else if (name == "three_material_ball_with_defocus_blur")
     three_material_ball_with_defocus_blur(width, aspect, out);
+  else if (name == "sponza")
+    sponza(width, aspect, out);
   else
     return false;
   return true;
@@ -173,7 +233,11 @@ void* rtsc_build(const char* name, int width, double aspect, rt_scene_desc* desc
     if (err && errlen > 0) std::snprintf(err, (size_t)errlen, "%s", m.c_str());
     return nullptr;
   };
-  if (!name || !build_config_scene(name, width, aspect, &h->scene)) return fail("unknown scene");
+  try {
+    if (!name || !build_config_scene(name, width, aspect, &h->scene)) return fail("unknown scene");
+  } catch (const std::exception& e) {
+    return fail(e.what());
+  }
   try {
     int w = h->sb.add(*h->scene.world);
     int l = h->scene.light ? h->sb.add(*h->scene.light) : -1;
@@ -190,6 +254,23 @@ void* rtsc_build(const char* name, int width, double aspect, rt_scene_desc* desc
 }
 
 void rtsc_free(void* h) { delete static_cast<rtsc_handle*>(h); }
+
+// The triangles main.cc's sponza() builds from a glTF file (gltf_loader.h + main.cc:447-485):
+// up to `cap` triangles as 9 doubles each into `xyz` (may be null); returns the total count,
+// or -1 with the message in err.
+long long rtsc_gltf_triangles(const char* path, double* xyz, long long cap, char* err, int errlen) {
+  try {
+    gltf::GltfLoader model(path ? path : "");
+    auto tris = gltf_triangles(model.getOutputPrimitives());
+    for (long long i = 0; i < (long long)tris.size() && i < cap && xyz; i++)
+      for (int v = 0; v < 3; v++)
+        for (int k = 0; k < 3; k++) xyz[9 * i + 3 * v + k] = tris[(size_t)i][v][k];
+    return (long long)tris.size();
+  } catch (const std::exception& e) {
+    if (err && errlen > 0) std::snprintf(err, (size_t)errlen, "%s", e.what());
+    return -1;
+  }
+}
 
 // The full drop-in path: build the scene, camera::render(of, world, light) to a PPM file.
 int rtsc_render_ppm(const char* name, int width, double aspect, int spp, int max_depth, uint64_t seed, int precision,

@@ -1,6 +1,7 @@
 // config_scenes.h -- the reference's main.cc scenes that BASELINE.json's configs
 // use, written against the plugin surface exactly as a main.cc caller would.
 #pragma once
+#include <array>
 #include <memory>
 #include <string>
 
@@ -18,6 +19,8 @@ struct config_scene {
   camera cam;
 };
 
-// name: cornell_box | cornell_box_with_volume | rtow | rtow_motion | three_material_ball.
-// width/aspect <= 0 keep the scene's own camera. Returns false for an unknown name.
+// name: cornell_box | cornell_box_with_volume | rtow | rtow_motion | three_material_ball |
+// three_material_ball_with_defocus_blur | sponza ($RT_SPONZA_GLTF or ./assets/Sponza/glTF/Sponza.gltf).
+// width/aspect <= 0 keep the scene's own camera. Returns false for an unknown name; throws
+// std::runtime_error when a scene's asset cannot be loaded.
 bool build_config_scene(const std::string& name, int width, double aspect, config_scene* out);
