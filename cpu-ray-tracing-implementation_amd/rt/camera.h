@@ -134,6 +134,20 @@ class camera {
     return true;
   }
 
+  // image_ as a Portable Float Map (linear, lossless; little-endian, bottom row first).
+  bool write_pfm(const std::string& path) const {
+    std::ofstream f(path, std::ios::binary);
+    if (!f) return false;
+    f << "PF\n" << image_width_ << ' ' << image_height_ << "\n-1.0\n";
+    for (int y = image_height_ - 1; y >= 0; y--)
+      for (int x = 0; x < image_width_; x++) {
+        const color& c = image_[(size_t)y * image_width_ + x];
+        const float v[3] = {(float)c.x(), (float)c.y(), (float)c.z()};
+        f.write(reinterpret_cast<const char*>(v), sizeof v);
+      }
+    return bool(f);
+  }
+
   // The camera as the C ABI sees it (the values initialize_* computed).
   rt_camera_desc describe() const {
     rt_camera_desc c{};

@@ -52,3 +52,15 @@ def test_example_main_fails_cleanly_without_gpu(tmp_path):
     r = subprocess.run([exe, "--scene", "cornell_box", "--width", "8", "--spp", "1", "--out", str(tmp_path / "x.ppm")],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and "render failed" in r.stderr
+
+
+def test_output_writers_match_the_reference_ppm(tmp_path):
+    # rt_amd.output.write_ppm == the reference's write_color text (oracle restatement), incl. values > 1
+    from rt_amd import output
+    rng = np.random.default_rng(5)
+    img = rng.uniform(-0.2, 3.0, size=(7, 5, 3))
+    img[0, 0] = [np.nan, 0.0, 1e-9]
+    assert output.ppm_bytes(img) == oracle.ppm(img)
+    output.write_pfm(img.astype(np.float32), str(tmp_path / "a.pfm"))
+    back = output.read_pfm(str(tmp_path / "a.pfm"))
+    np.testing.assert_array_equal(np.nan_to_num(back, nan=-7), np.nan_to_num(img.astype(np.float32), nan=-7))
