@@ -219,6 +219,8 @@ struct DevScene {
   int32_t background;
   int32_t has_volumes;
   uint32_t n_nodes;
+  const double* texdata;  // procedural-texture tables (Texture::data)
+  int32_t has_procedural; // any perlin / value / worley / voronoi texture: the EXT kernels
 };
 
 // World -> object through an instance chain (hittable.h:75-82, 125-135, 192-202, 259-270).
@@ -737,12 +739,119 @@ __device__ __forceinline__ void trace_linear(const DevScene<R>& sc, V<R> wo, V<R
 }
 
 // ------------------------------------------------------------------ textures, pdfs
-template <class R>
-__device__ __forceinline__ V<R> tex_sample(const Texture<R>& tx, V<R> p) {  // texture.h:15,47-56
-  if (tx.kind == T_SOLID) return ld3(tx.c0);
-  V<R> uv = p / tx.scale;
-  int total = (int)floor(uv.x) + (int)floor(uv.y) + (int)floor(uv.z);
-  return (total % 2 == 0) ? ld3(tx.c1) : ld3(tx.c0);
+// ---- procedural noise (noise.h), in fp64 for both paths: the sin hashes of worley/voronoi
+// pick different cells in fp32, and the reference evaluates all of it in double.
+// perlin::noise / perlin_interp (noise.h:22-42, 56-68); tb = rand_offset[256][3], perm_x[256]
+__device__ __forceinline__ double perlin_noise(const double* tb, double px, double py, double pz) {
+#pragma clang fp contract(off)  // the reference's rounding: the sin hash amplifies any FMA
+  int iu = (int)floor(px), iv = (int)floor(py), iw = (int)floor(pz);
+  const double u = px - iu, v = py - iv, w = pz - iw;
+  iu &= 255;
+  iv &= 255;
+  iw &= 255;
+  const double* perm = tb + 3 * kPerlinPoints;
+  const double uu = u * u * (3 - 2 * u), vv = v * v * (3 - 2 * v), ww = w * w * (3 - 2 * w);
+  double accum = 0.0;
+  for (int i = 0; i < 2; i++)
+    for (int j = 0; j < 2; j++)
+      for (int k = 0; k < 2; k++) {
+        // perm_x for all three axes, as the reference (noise.h:36)
+        const int g = (int)perm[(iu + i) % 256] ^ (int)perm[(iv + j) % 256] ^ (int)perm[(iw + k) % 256];
+        const double* r = tb + 3 * g;
+        const double d = r[0] * (u - i) + r[1] * (v - j) + r[2] * (w - k);
+        accum += (i * uu + (1 - i) * (1 - uu)) * (j * vv + (1 - j) * (1 - vv)) * (k * ww + (1 - k) * (1 - ww)) * d;
+      }
+  return accum;
+}
+// perlin_texture::sample (texture.h:84-88) with turb(7, p / scale) (noise.h:44-54)
+__device__ __forceinline__ double perlin_texture(const double* tb, double scale, double px, double py, double pz) {
+#pragma clang fp contract(off)  // the reference's rounding: the sin hash amplifies any FMA
+  double qx = px / scale, qy = py / scale, qz = pz / scale;
+  double accum = 0, weight = 1.0;
+  for (int i = 0; i < 7; i++) {
+    accum += weight * perlin_noise(tb, qx, qy, qz);
+    weight *= 0.5;
+    qx *= 2.0;
+    qy *= 2.0;
+    qz *= 2.0;
+  }
+  return .5 * (1 + sin(px + 70 * fabs(accum)));
+}
+// value_noise::noise (noise.h:109-131): trilinear over a float table indexed without wrapping;
+// an index outside the table (undefined behaviour in the reference) reads 0
+__device__ __forceinline__ double value_noise(const double* tb, uint32_t n, double px, double py, double pz) {
+#pragma clang fp contract(off)  // the reference's rounding: the sin hash amplifies any FMA
+  const double fx = floor(px), fy = floor(py), fz = floor(pz);
+  const double nn = (double)n, n3 = nn * nn * nn;
+  auto at = [&](double ix, double iy, double iz) -> double {
+    const double k = ix * nn * nn + iy * nn + iz;
+    return (k >= 0 && k < n3) ? (double)(float)tb[(size_t)k] : 0.0;
+  };
+  const double x000 = at(fx, fy, fz), x100 = at(fx + 1, fy, fz), x010 = at(fx, fy + 1, fz),
+               x110 = at(fx + 1, fy + 1, fz), x001 = at(fx, fy, fz + 1), x101 = at(fx + 1, fy, fz + 1),
+               x011 = at(fx, fy + 1, fz + 1), x111 = at(fx + 1, fy + 1, fz + 1);
+  const double x = px - fx, y = py - fy, z = pz - fz;
+  auto lerp = [](double t, double a, double b) { return (1 - t) * a + t * b; };  // utility.h:84
+  const double y0z0 = lerp(x, x000, x100), y1z0 = lerp(x, x010, x110), y0z1 = lerp(x, x001, x101),
+               y1z1 = lerp(x, x011, x111);
+  return lerp(z, lerp(y, y0z0, y1z0), lerp(y, y0z1, y1z1));
+}
+// worley_noise / voronoi_noise get_rand_offset (noise.h:141-145, 172-176)
+__device__ __forceinline__ void cell_hash(double ux, double uy, double uz, double& hx, double& hy, double& hz) {
+#pragma clang fp contract(off)  // the reference's rounding: the sin hash amplifies any FMA
+  const double ax = ux * 127.1 + uy * 311.7 + uz * 74.7;
+  const double ay = ux * 269.5 + uy * 183.3 + uz * 246.1;
+  const double az = ux * 113.5 + uy * 271.9 + uz * 307.7;
+  const double sx = sin(ax) * 43758.5453, sy = sin(ay) * 43758.5453, sz = sin(az) * 43758.5453;
+  hx = sx - floor(sx);
+  hy = sy - floor(sy);
+  hz = sz - floor(sz);
+}
+// noise.h:147-167 (worley: squared distance to the nearest feature point) and 178-200 (voronoi:
+// a hash of the nearest feature point), float distances as in the reference
+__device__ __forceinline__ double cell_noise(bool voronoi, double px, double py, double pz) {
+#pragma clang fp contract(off)  // the reference's rounding: the sin hash amplifies any FMA
+  const double fx = floor(px), fy = floor(py), fz = floor(pz);
+  float min_dist = 3.40282347e+38f, color = 0.0f;
+  for (int i = -1; i <= 1; i++)
+    for (int j = -1; j <= 1; j++)
+      for (int k = -1; k <= 1; k++) {
+        const double cx = fx + i, cy = fy + j, cz = fz + k;
+        double hx, hy, hz;
+        cell_hash(cx, cy, cz, hx, hy, hz);
+        const double qx = cx + hx, qy = cy + hy, qz = cz + hz;
+        const double dx = qx - px, dy = qy - py, dz = qz - pz;
+        const float dist = (float)sqrt(dx * dx + dy * dy + dz * dz);
+        if (dist < min_dist) {
+          min_dist = dist;
+          if (voronoi) {
+            double gx, gy, gz;
+            cell_hash(qx, qy, qz, gx, gy, gz);
+            color = (float)gx;
+          }
+        }
+      }
+  return voronoi ? (double)color : (double)(min_dist * min_dist);
+}
+
+// EXT: the kernel instantiation for scenes with procedural textures (or non-perspective
+// cameras); the base kernels only contain the solid and checker textures.
+template <class R, bool EXT>
+__device__ __forceinline__ V<R> tex_sample(const DevScene<R>& sc, const Texture<R>& tx, V<R> p) {  // texture.h
+  if (!EXT || tx.kind == T_SOLID || tx.kind == T_CHECKER) {
+    if (tx.kind == T_SOLID) return ld3(tx.c0);  // texture.h:15
+    V<R> uv = p / tx.scale;                     // texture.h:47-56
+    int total = (int)floor(uv.x) + (int)floor(uv.y) + (int)floor(uv.z);
+    return (total % 2 == 0) ? ld3(tx.c1) : ld3(tx.c0);
+  }
+  double g;
+  if (tx.kind == T_PERLIN)
+    g = perlin_texture(sc.texdata + tx.data, (double)tx.scale, p.x, p.y, p.z);
+  else if (tx.kind == T_VALUE)
+    g = value_noise(sc.texdata + tx.data, tx.n, p.x, p.y, p.z);
+  else
+    g = cell_noise(tx.kind == T_VORONOI, p.x, p.y, p.z);
+  return mkv(R(g), R(g), R(g));  // color(noise) (texture.h:99, 107, 115)
 }
 
 template <class R>

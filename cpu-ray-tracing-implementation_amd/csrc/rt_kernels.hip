@@ -275,7 +275,7 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
     if (sc.background >= 0) {
       R tb;
       if (sphere_roots<R>(o.x, o.y, o.z, d.x, d.y, d.z, o.x, o.y, o.z, R(1), R(0.001), Num<R>::inf(), false, tb)) {
-        add = s.thr * tex_sample(sc.texs[sc.background], o + tb * d);
+        add = s.thr * tex_sample<R, CAMX>(sc, sc.texs[sc.background], o + tb * d);
         has_add = true;
       }
     }
@@ -361,12 +361,12 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
     const Material<R>& m = sc.mats[mat];
     if (m.kind == M_DIFFUSE_LIGHT) {  // material.h:211-215; no scatter
       if (front) {
-        add = s.thr * tex_sample(m.tx, pw);
+        add = s.thr * tex_sample<R, CAMX>(sc, m.tx, pw);
         has_add = true;
       }
       done = true;
     } else {
-      V<R> att = tex_sample(m.tx, pw);
+      V<R> att = tex_sample<R, CAMX>(sc, m.tx, pw);
       const uint32_t bounce = (uint32_t)s.bounce;
       uint32_t js = 0;
       auto U = [&]() { return to_unit<R>(draw_u32(s.ks, dim_scatter(bounce, js++))); };
@@ -584,7 +584,8 @@ __device__ __forceinline__ void step_body(const Params<R>& p) {
 
 // The kernel; k_step_occ is the same body with the register budget cut for Trav::kWaves
 // waves per SIMD (only where that does not spill much, see LinearTrav::kWaves).
-// CAMX: the camera is not perspective (camera_ray); the perspective kernels do not contain it.
+// CAMX ("extended"): a non-perspective camera (camera_ray) or procedural textures (noise.h); the
+// base kernels, which every BASELINE config except the noise scenes uses, contain neither.
 template <class R, class Trav, bool CAMX>
 __global__ __launch_bounds__(kBlock) void k_step(Params<R> p) {
   step_body<R, Trav, CAMX>(p);
@@ -814,23 +815,21 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
   s.background = h.background;
   s.has_volumes = h.has_volumes;
   s.n_nodes = h.n_nodes;
+  s.texdata = (const double*)at(h.off_texdata);
+  s.has_procedural = h.n_texdata > 0 || h.has_cell_noise;
   return s;
 }
 
 template <class R, class Trav>
 void launch_k(const Params<R>& p, uint32_t grid, hipStream_t st) {
-  const bool camx = p.cam_mode != RT_CAM_PERSPECTIVE;
-  if constexpr (Trav::kWaves > 1) {
-    if (camx)
-      hipLaunchKernelGGL((k_step_occ<R, Trav, true>), dim3(grid), dim3(kBlock), 0, st, p);
-    else
-      hipLaunchKernelGGL((k_step_occ<R, Trav, false>), dim3(grid), dim3(kBlock), 0, st, p);
-  } else {
-    if (camx)
-      hipLaunchKernelGGL((k_step<R, Trav, true>), dim3(grid), dim3(kBlock), 0, st, p);
-    else
-      hipLaunchKernelGGL((k_step<R, Trav, false>), dim3(grid), dim3(kBlock), 0, st, p);
-  }
+  const bool camx = p.cam_mode != RT_CAM_PERSPECTIVE || p.sc.has_procedural;
+  // the extended kernels run without the occupancy budget (their noise / camera code would spill)
+  if (camx)
+    hipLaunchKernelGGL((k_step<R, Trav, true>), dim3(grid), dim3(kBlock), 0, st, p);
+  else if constexpr (Trav::kWaves > 1)
+    hipLaunchKernelGGL((k_step_occ<R, Trav, false>), dim3(grid), dim3(kBlock), 0, st, p);
+  else
+    hipLaunchKernelGGL((k_step<R, Trav, false>), dim3(grid), dim3(kBlock), 0, st, p);
 }
 
 template <class R>
@@ -946,7 +945,7 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     const int K = prm->segments_per_launch > 0 ? std::min(prm->segments_per_launch, 64) : kAutoSegments;
     p.K = K;
 
-    if (p.cam_mode != RT_CAM_PERSPECTIVE)
+    if (p.cam_mode != RT_CAM_PERSPECTIVE || p.sc.has_procedural)
       hipLaunchKernelGGL((k_init<R, true>), dim3(nblk_max), dim3(kBlock), 0, st, p);
     else
       hipLaunchKernelGGL((k_init<R, false>), dim3(nblk_max), dim3(kBlock), 0, st, p);

@@ -152,6 +152,8 @@ class Compiler {
   std::vector<Node<double>> nodes_;
   std::vector<uint32_t> refs_;
   std::vector<Material<double>> mats_;
+  std::vector<double> texdata_;  // procedural-texture tables (Texture::data offsets)
+  bool cell_noise_ = false;      // a worley / voronoi texture
   std::vector<int32_t> mat_remap_;                    // descriptor material -> mats_ index
   std::unordered_map<std::string, int32_t> mat_index_;  // material record bytes -> mats_ index
   int32_t mat_id(int32_t m) const { return mat_remap_[(size_t)m]; }
@@ -692,6 +694,8 @@ Texture<float> to32(const Texture<double>& t) {
   r.kind = t.kind;
   cvt3(r.c1, t.c1);
   r.scale = (float)t.scale;
+  r.data = t.data;
+  r.n = t.n;
   return r;
 }
 Light<float> to32(const Light<double>& l) {
@@ -718,7 +722,7 @@ template <class Q, class S, class T, class I, class V, class N, class M, class X
 SceneHeader pack(std::vector<unsigned char>& blob, const std::vector<Q>& q, const std::vector<S>& s,
                  const std::vector<T>& t, const std::vector<I>& in, const std::vector<V>& vo, const std::vector<N>& nd,
                  const std::vector<uint32_t>& refs, const std::vector<M>& m, const std::vector<X>& x, const L& light,
-                 const std::vector<LR>& linear) {
+                 const std::vector<LR>& linear, const std::vector<double>& texdata) {
   SceneHeader h{};
   blob.clear();
   h.off_quads = append(blob, q);
@@ -733,6 +737,8 @@ SceneHeader pack(std::vector<unsigned char>& blob, const std::vector<Q>& q, cons
   h.off_light = append(blob, std::vector<L>{light});
   h.off_linear = append(blob, linear);
   h.n_linear = (uint32_t)linear.size();
+  h.off_texdata = append(blob, texdata);
+  h.n_texdata = texdata.size();
   blob.resize((blob.size() + 255) & ~size_t(255));
   h.bytes = blob.size();
   h.n_quads = (uint32_t)q.size();
@@ -824,6 +830,39 @@ bool Compiler::run(CompiledScene* out, std::string* err) {
         r.c1[k] = t.even[k];
       }
       r.scale = t.scale;
+    } else if (t.kind == RT_TEX_PERLIN) {  // texture.h:80-92: the tables perlin's constructor drew
+      const int64_t need = 3 * kPerlinPoints + 3 * kPerlinPoints;  // rand_offset, perm_x, perm_y, perm_z
+      if (!d_->tex_data || t.data < 0 || (int64_t)t.data + need > d_->num_tex_data) {
+        *err = "perlin texture " + std::to_string(i) + ": tex_data too short";
+        return false;
+      }
+      const double* src = d_->tex_data + t.data;
+      r.kind = T_PERLIN;
+      r.scale = t.scale;
+      r.data = (uint32_t)texdata_.size();
+      texdata_.insert(texdata_.end(), src, src + 3 * kPerlinPoints);  // rand_offset
+      for (uint32_t k = 0; k < kPerlinPoints; k++) {  // perm_x: the only one noise.h:36 reads
+        const double v = src[3 * kPerlinPoints + k];
+        if (!(v >= 0 && v < kPerlinPoints)) {
+          *err = "perlin texture " + std::to_string(i) + ": permutation entry out of range";
+          return false;
+        }
+        texdata_.push_back(v);
+      }
+    } else if (t.kind == RT_TEX_VALUE) {  // texture.h:95-103: n^3 values
+      const double n = t.scale;
+      if (!(n >= 1 && n <= 1024 && n == (double)(int64_t)n) || !d_->tex_data || t.data < 0 ||
+          (int64_t)t.data + (int64_t)(n * n * n) > d_->num_tex_data) {
+        *err = "value texture " + std::to_string(i) + ": bad resolution or tex_data too short";
+        return false;
+      }
+      r.kind = T_VALUE;
+      r.n = (uint32_t)n;
+      r.data = (uint32_t)texdata_.size();
+      texdata_.insert(texdata_.end(), d_->tex_data + t.data, d_->tex_data + t.data + (int64_t)(n * n * n));
+    } else if (t.kind == RT_TEX_WORLEY || t.kind == RT_TEX_VORONOI) {  // stateless (noise.h:139-201)
+      r.kind = t.kind == RT_TEX_WORLEY ? T_WORLEY : T_VORONOI;
+      cell_noise_ = true;
     } else {
       *err = "texture kind " + std::to_string(t.kind) + " is not implemented on the device";
       return false;
@@ -857,6 +896,8 @@ bool Compiler::run(CompiledScene* out, std::string* err) {
     put(r.tx.c0, 24);
     put(r.tx.c1, 24);
     put(&r.tx.scale, 8);
+    put(&r.tx.data, 4);
+    put(&r.tx.n, 4);
     auto it = mat_index_.find(key);
     if (it == mat_index_.end()) {
       it = mat_index_.emplace(key, (int32_t)mats_.size()).first;
@@ -898,10 +939,12 @@ bool Compiler::run(CompiledScene* out, std::string* err) {
   out->stack_need = std::max(1, root.need);
   out->bvh_depth = root.depth;
   out->num_items = (int)top.size();
-  out->hdr64 = pack(out->blob64, quads_, spheres_, tris_, insts_, vols_, nodes_, refs_, mats_, texs_, light_, linear);
+  out->hdr64 =
+      pack(out->blob64, quads_, spheres_, tris_, insts_, vols_, nodes_, refs_, mats_, texs_, light_, linear, texdata_);
   out->hdr = pack(out->blob32, map32(quads_), map32(spheres_), map32(tris_), map32(insts_), map32(vols_),
-                  map32(nodes_), refs_, map32(mats_), map32(texs_), to32(light_), map32(linear));
+                  map32(nodes_), refs_, map32(mats_), map32(texs_), to32(light_), map32(linear), texdata_);
   for (SceneHeader* h : {&out->hdr, &out->hdr64}) {
+    h->has_cell_noise = cell_noise_ ? 1 : 0;
     h->root = root.entry;
     h->background = d_->background;
     h->has_volumes = vols_.empty() ? 0 : 1;

@@ -22,9 +22,10 @@ RT_OBJ_SPHERE, RT_OBJ_QUAD, RT_OBJ_TRIANGLE, RT_OBJ_LIST, RT_OBJ_BVH, RT_OBJ_TRA
     RT_OBJ_ROTATE_Y, RT_OBJ_ROTATE_Z, RT_OBJ_VOLUME = range(1, 11)
 # rt_material_kind
 RT_MAT_LAMBERTIAN, RT_MAT_METAL, RT_MAT_DIELECTRIC, RT_MAT_ISOTROPIC, RT_MAT_DIFFUSE_LIGHT, RT_MAT_GLOSS = range(1, 7)
-RT_TEX_SOLID, RT_TEX_CHECKER = 1, 2
+RT_TEX_SOLID, RT_TEX_CHECKER, RT_TEX_PERLIN, RT_TEX_VALUE, RT_TEX_WORLEY, RT_TEX_VORONOI = range(1, 7)
 RT_CAM_PERSPECTIVE, RT_CAM_ORTHONORMAL, RT_CAM_FISHEYE, RT_CAM_LENS = range(4)
 RT_PREC_F32, RT_PREC_F64 = 0, 1
+ABI_VERSION = 2  # include/rt_hip.h RT_ABI_VERSION
 
 
 class rt_object(ctypes.Structure):
@@ -39,7 +40,7 @@ class rt_material(ctypes.Structure):
 
 
 class rt_texture(ctypes.Structure):
-    _fields_ = [("kind", c_int32), ("pad_", c_int32), ("color", D3), ("odd", D3), ("even", D3), ("scale", c_double)]
+    _fields_ = [("kind", c_int32), ("data", c_int32), ("color", D3), ("odd", D3), ("even", D3), ("scale", c_double)]
 
 
 class rt_scene_desc(ctypes.Structure):
@@ -47,7 +48,8 @@ class rt_scene_desc(ctypes.Structure):
                 ("children", ctypes.POINTER(c_int32)), ("num_children", c_int32),
                 ("materials", ctypes.POINTER(rt_material)), ("num_materials", c_int32),
                 ("textures", ctypes.POINTER(rt_texture)), ("num_textures", c_int32),
-                ("world", c_int32), ("light", c_int32), ("background", c_int32), ("pad_", c_int32)]
+                ("world", c_int32), ("light", c_int32), ("background", c_int32), ("pad_", c_int32),
+                ("tex_data", ctypes.POINTER(c_double)), ("num_tex_data", ctypes.c_int64)]
 
 
 class rt_camera_desc(ctypes.Structure):
@@ -114,6 +116,8 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        if lib.rt_abi_version() != ABI_VERSION:
+            raise RuntimeError(f"{path} has ABI {lib.rt_abi_version()}, this binding expects {ABI_VERSION}: rebuild")
         _lib = lib
     return _lib
 

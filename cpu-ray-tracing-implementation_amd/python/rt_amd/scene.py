@@ -13,8 +13,17 @@ from . import abi
 
 
 class SceneBuilder:
-    def __init__(self):
+    def __init__(self, rand=None):
+        """rand: the uniform [0,1) source procedural textures draw their tables from (the
+        reference's random_double, utility.h:20); default: glibc rand(), as the reference."""
         self.objects, self.children, self.materials, self.textures = [], [], [], []
+        self.tex_data = []
+        if rand is None:
+            import ctypes
+            libc = ctypes.CDLL(None)
+            libc.rand.restype = ctypes.c_int
+            rand = lambda: libc.rand() / (2147483647 + 1.0)
+        self._rand = rand
 
     # textures (texture.h:12-63)
     def solid(self, color):
@@ -28,6 +37,45 @@ class SceneBuilder:
         t.odd[:] = [float(c) for c in odd]
         t.even[:] = [float(c) for c in even]
         self.textures.append(t)
+        return len(self.textures) - 1
+
+    # procedural textures (texture.h:80-119, noise.h): tables drawn as the constructors draw them
+    def _emit_data(self, values):
+        off = len(self.tex_data)
+        self.tex_data.extend(float(v) for v in values)
+        return off
+
+    def perlin(self, scale):
+        rd = self._rand
+        offsets = []
+        for _ in range(256):  # unit_vector(random_vec(-1, 1)): GCC evaluates vec3(...) right to left
+            z, y, x = (-1 + 2 * rd() for _ in range(3))
+            n = math.sqrt(x * x + y * y + z * z)
+            offsets += [x / n, y / n, z / n]
+        perms = []
+        for _ in range(3):  # perm_x, perm_y, perm_z: Fisher-Yates with random_int(0, i) (noise.h:82-97)
+            p = list(range(256))
+            for i in range(255, 0, -1):
+                t = int(0 + (i - 0) * rd())
+                p[i], p[t] = p[t], p[i]
+            perms += p
+        t = abi.rt_texture(kind=abi.RT_TEX_PERLIN, scale=float(scale), data=self._emit_data(offsets + perms))
+        self.textures.append(t)
+        return len(self.textures) - 1
+
+    def value(self, resolution):
+        rd = self._rand
+        vals = [float(np.float32(rd())) for _ in range(resolution ** 3)]  # std::vector<float> (noise.h:135)
+        t = abi.rt_texture(kind=abi.RT_TEX_VALUE, scale=float(resolution), data=self._emit_data(vals))
+        self.textures.append(t)
+        return len(self.textures) - 1
+
+    def worley(self):
+        self.textures.append(abi.rt_texture(kind=abi.RT_TEX_WORLEY))
+        return len(self.textures) - 1
+
+    def voronoi(self):
+        self.textures.append(abi.rt_texture(kind=abi.RT_TEX_VORONOI))
         return len(self.textures) - 1
 
     # materials (material.h)
@@ -119,8 +167,10 @@ class SceneBuilder:
             (abi.c_int32 * max(1, len(self.children)))(*self.children),
             (abi.rt_material * max(1, len(self.materials)))(*self.materials),
             (abi.rt_texture * max(1, len(self.textures)))(*self.textures),
+            (abi.c_double * max(1, len(self.tex_data)))(*self.tex_data),
         )
-        d.objects, d.children, d.materials, d.textures = self._keep
+        d.objects, d.children, d.materials, d.textures, d.tex_data = self._keep
+        d.num_tex_data = len(self.tex_data)
         d.num_objects, d.num_children = len(self.objects), len(self.children)
         d.num_materials, d.num_textures = len(self.materials), len(self.textures)
         d.world, d.light, d.background = world, light, background

@@ -46,6 +46,12 @@ class scene_builder {
     textures_.push_back(t);
     return (int)textures_.size() - 1;
   }
+  // procedural-texture tables; returns their offset for rt_texture.data
+  int32_t emit_tex_data(const std::vector<double>& v) {
+    const int32_t off = (int32_t)tex_data_.size();
+    tex_data_.insert(tex_data_.end(), v.begin(), v.end());
+    return off;
+  }
 
   rt_scene_desc desc(int world, int light, int background) const {
     rt_scene_desc d{};
@@ -60,6 +66,8 @@ class scene_builder {
     d.world = world;
     d.light = light;
     d.background = background;
+    d.tex_data = tex_data_.empty() ? nullptr : tex_data_.data();
+    d.num_tex_data = (int64_t)tex_data_.size();
     return d;
   }
 
@@ -81,5 +89,6 @@ class scene_builder {
   std::vector<int32_t> children_;
   std::vector<rt_material> materials_;
   std::vector<rt_texture> textures_;
+  std::vector<double> tex_data_;
   std::unordered_map<const void*, int> seen_obj_, seen_mat_, seen_tex_;
 };

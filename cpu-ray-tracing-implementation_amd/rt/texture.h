@@ -1,10 +1,11 @@
-// texture.h -- textures of the plugin surface (reference: src/texture.h:6-63).
-// solid_color and checker_texture run on the device; a texture subclass the
-// device does not know makes camera::render fail with unsupported_object.
+// texture.h -- textures of the plugin surface (reference: src/texture.h:6-119).
+// solid_color, checker_texture and the procedural noise textures run on the device; a texture
+// subclass the device does not know makes camera::render fail with unsupported_object.
 #pragma once
 #include <memory>
 
 #include "color.h"
+#include "noise.h"
 #include "ray.h"
 #include "scene_builder.h"
 
@@ -69,4 +70,66 @@ class checker_texture : public texture {
  private:
   color odd_, even_;
   double scale_;
+};
+
+// 0.5 (1 + sin(p.x + 70 turb(7, p / scale))) in every channel (texture.h:80-92)
+class perlin_texture : public texture {
+ public:
+  explicit perlin_texture(double scale) : scale_(scale) {}
+  color sample(double, double, point3 p) override {
+    return color(.5, .5, .5) * (1 + std::sin((p.x() + 70 * noise_.turb(7, p / scale_))));
+  }
+  int flatten(scene_builder& sb) const override {
+    rt_texture t{};
+    t.kind = RT_TEX_PERLIN;
+    t.scale = scale_;
+    t.data = sb.emit_tex_data(noise_.tables());
+    return sb.emit_texture(t);
+  }
+
+ private:
+  perlin noise_;
+  double scale_;
+};
+
+class value_texture : public texture {  // texture.h:95-103
+ public:
+  explicit value_texture(int resolution) : noise_(resolution) {}
+  color sample(double, double, point3 p) override { return color(noise_.noise(p)); }
+  int flatten(scene_builder& sb) const override {
+    rt_texture t{};
+    t.kind = RT_TEX_VALUE;
+    t.scale = noise_.resolution();
+    t.data = sb.emit_tex_data(noise_.tables());
+    return sb.emit_texture(t);
+  }
+
+ private:
+  value_noise noise_;
+};
+
+class worley_texture : public texture {  // texture.h:105-111
+ public:
+  color sample(double, double, point3 p) override { return color(noise_.noise(p)); }
+  int flatten(scene_builder& sb) const override {
+    rt_texture t{};
+    t.kind = RT_TEX_WORLEY;
+    return sb.emit_texture(t);
+  }
+
+ private:
+  worley_noise noise_;
+};
+
+class voronoi_texture : public texture {  // texture.h:113-119
+ public:
+  color sample(double, double, point3 p) override { return color(noise_.noise(p)); }
+  int flatten(scene_builder& sb) const override {
+    rt_texture t{};
+    t.kind = RT_TEX_VORONOI;
+    return sb.emit_texture(t);
+  }
+
+ private:
+  voronoi_noise noise_;
 };

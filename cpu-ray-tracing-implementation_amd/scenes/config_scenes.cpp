@@ -141,6 +141,44 @@ void three_material_ball_with_defocus_blur(int width, double aspect, config_scen
   s->cam.background_ = std::make_shared<solid_color>(color(0.7, 0.8, 1.0));
 }
 
+// main.cc:581-630: a 10 x 10 or 40 x 40 quad under an orthonormal camera, white background
+void noise_quad(std::shared_ptr<texture> tex, double size, double view, int width, double aspect,
+                config_scene* s) {
+  auto world = std::make_shared<hittable_list>();
+  world->push_back(std::make_shared<quad>(point3(0, 0, 0), vec3(size, 0, 0), vec3(0, size, 0),
+                                          std::make_shared<lambertian>(tex)));
+  s->world = world;
+  s->cam.initialize_orthnormal(W(width, 400), A(aspect, 1), view, vec3(size / 2, size / 2, 1),
+                               vec3(size / 2, size / 2, 0), 10, 5);
+  s->cam.background_ = solid_color::white;
+}
+
+void perlin_texture_ball(int width, double aspect, config_scene* s) {  // main.cc:402-437
+  hittable_list boxes1;
+  auto ground = std::make_shared<lambertian>(color(0.48, 0.83, 0.53));
+  for (int i = 0; i < 20; i++)
+    for (int j = 0; j < 20; j++) {
+      double w = 100.0, x0 = -1000.0 + i * w, z0 = -1000.0 + j * w, y0 = 0.0;
+      double x1 = x0 + w, y1 = random_double(1, 101), z1 = z0 + w;
+      boxes1.push_back(box(point3(x0, y0, z0), point3(x1, y1, z1), ground));
+    }
+  auto world = std::make_shared<hittable_list>();
+  world->push_back(std::make_shared<bvh_node>(boxes1));
+  auto light = std::make_shared<diffuse_light>(color(7, 7, 7));
+  auto quad_light = std::make_shared<quad>(point3(123, 554, 147), vec3(300, 0, 0), vec3(0, 0, 265), light);
+  world->push_back(quad_light);
+  world->push_back(std::make_shared<sphere>(point3(260, 150, 45), 50, std::make_shared<dielectric>(1.5)));
+  auto pertext = std::make_shared<perlin_texture>(8);
+  world->push_back(std::make_shared<translate>(
+      point3(180, 280, 400),
+      std::make_shared<rotate_x>(std::make_shared<sphere>(point3(0), 80, std::make_shared<lambertian>(pertext)),
+                                 -90)));
+  s->cam.initialize_perspective(W(width, 600), A(aspect, 1.0), point3(478, 278, -600), point3(278, 278, 0), 1,
+                                40.0, 500, 5);
+  s->world = std::make_shared<bvh_node>(*world);
+  // cam.render(of, bvh): the light is not importance-sampled in this scene (main.cc:436)
+}
+
 // main.cc:447-485: the triangles sponza() builds from the loader's output primitives -- float
 // positions only, uint16 indices only (other index types leave the primitive empty), and
 // consecutive position triples when a primitive has no indices.
@@ -211,6 +249,16 @@ bool build_config_scene(const std::string& name, int width, double aspect, confi
     three_material_ball_with_defocus_blur(width, aspect, out);
   else if (name == "sponza")
     sponza(width, aspect, out);
+  else if (name == "perlin_texture_ball")
+    perlin_texture_ball(width, aspect, out);
+  else if (name == "test_perlin_noise")
+    noise_quad(std::make_shared<perlin_texture>(1), 10, 10, width, aspect, out);
+  else if (name == "test_value_noise")
+    noise_quad(std::make_shared<value_texture>(40), 40, 20, width, aspect, out);
+  else if (name == "test_worley_noise")
+    noise_quad(std::make_shared<worley_texture>(), 40, 20, width, aspect, out);
+  else if (name == "test_voronoi_noise")
+    noise_quad(std::make_shared<voronoi_texture>(), 40, 20, width, aspect, out);
   else
     return false;
   return true;

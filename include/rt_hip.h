@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 typedef enum rt_status {
   RT_OK = 0,
@@ -100,17 +100,22 @@ typedef struct rt_material {
 } rt_material;
 
 typedef enum rt_texture_kind {
-  RT_TEX_SOLID = 1,  /* texture.h:12-37 */
-  RT_TEX_CHECKER = 2 /* texture.h:39-63 */
+  RT_TEX_SOLID = 1,   /* texture.h:12-37 */
+  RT_TEX_CHECKER = 2, /* texture.h:39-63 */
+  RT_TEX_PERLIN = 3,  /* texture.h:80-92, noise.h:10-89. scale; tex_data[data ..]: rand_offset (256 x 3),
+                         then perm_x, perm_y, perm_z (256 each) as the constructor drew them */
+  RT_TEX_VALUE = 4,   /* texture.h:95-103, noise.h:95-137. scale = resolution n; tex_data[data ..]: n^3 values */
+  RT_TEX_WORLEY = 5,  /* texture.h:105-111, noise.h:139-168 */
+  RT_TEX_VORONOI = 6  /* texture.h:113-119, noise.h:170-201 */
 } rt_texture_kind;
 
 typedef struct rt_texture {
   int32_t kind;
-  int32_t pad_;
+  int32_t data;    /* perlin / value: offset of the texture's tables in rt_scene_desc.tex_data */
   double color[3]; /* solid */
   double odd[3];   /* checker */
   double even[3];  /* checker */
-  double scale;    /* checker */
+  double scale;    /* checker, perlin; value: the resolution */
 } rt_texture;
 
 typedef struct rt_scene_desc {
@@ -126,6 +131,8 @@ typedef struct rt_scene_desc {
   int32_t light;      /* object used for importance sampling, or -1 (camera.h:135 `light`) */
   int32_t background; /* texture index of camera::background_, or -1 (camera.h:329) */
   int32_t pad_;
+  const double* tex_data; /* procedural-texture tables (rt_texture.data), may be NULL */
+  int64_t num_tex_data;
 } rt_scene_desc;
 
 /* ---- camera: the values camera::initialize_* computes (camera.h:21-132) ---- */

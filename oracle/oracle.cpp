@@ -194,18 +194,110 @@ struct box3 {  // aabb.h
 };
 
 // ---------------------------------------------------------------- textures (texture.h)
+// noise.h:10-201 restated. perlin keeps the tables its constructor drew (rand_offset, perm_x;
+// perm_y/perm_z are drawn but never read: noise.h:36 indexes perm_x for all three axes).
+struct onoise {
+  std::vector<v3> rand_offset;   // perlin (256) -- noise.h:76-80
+  std::vector<int> perm_x;       // perlin
+  std::vector<float> values;     // value noise, resolution^3 (noise.h:134-136)
+  int resolution = 0;
+  double perlin(const v3& p) const {  // noise.h:56-68, 22-42
+    int iu = int(std::floor(p.x)), iv = int(std::floor(p.y)), iw = int(std::floor(p.z));
+    double u = p.x - iu, v = p.y - iv, w = p.z - iw;
+    iu = iu & 255;
+    iv = iv & 255;
+    iw = iw & 255;
+    double uu = u * u * (3 - 2 * u), vv = v * v * (3 - 2 * v), ww = w * w * (3 - 2 * w);
+    double accum = 0.0;
+    for (int i = 0; i < 2; i++)
+      for (int j = 0; j < 2; j++)
+        for (int k = 0; k < 2; k++) {
+          v3 weight(u - i, v - j, w - k);
+          const v3& g = rand_offset[perm_x[(iu + i) % 256] ^ perm_x[(iv + j) % 256] ^ perm_x[(iw + k) % 256]];
+          accum += (i * uu + (1 - i) * (1 - uu)) * (j * vv + (1 - j) * (1 - vv)) * (k * ww + (1 - k) * (1 - ww)) *
+                   dot(g, weight);
+        }
+    return accum;
+  }
+  double turb(int depth, const v3& p) const {  // noise.h:44-54
+    double accum = 0;
+    v3 q = p;
+    double weight = 1.0;
+    for (int i = 0; i < depth; i++) {
+      accum += weight * perlin(q);
+      weight *= 0.5;
+      q = q * 2.0;
+    }
+    return std::fabs(accum);
+  }
+  double value(const v3& p) const {  // noise.h:109-131; an index outside the table reads 0
+    double fx = std::floor(p.x), fy = std::floor(p.y), fz = std::floor(p.z);
+    double n = resolution, n3 = n * n * n;
+    auto at = [&](double x, double y, double z) -> float {
+      double k = x * n * n + y * n + z;
+      return (k >= 0 && k < n3) ? values[(size_t)k] : 0.0f;
+    };
+    float x000 = at(fx, fy, fz), x100 = at(fx + 1, fy, fz), x010 = at(fx, fy + 1, fz), x110 = at(fx + 1, fy + 1, fz);
+    float x001 = at(fx, fy, fz + 1), x101 = at(fx + 1, fy, fz + 1), x011 = at(fx, fy + 1, fz + 1),
+          x111 = at(fx + 1, fy + 1, fz + 1);
+    double x = p.x - fx, y = p.y - fy, z = p.z - fz;
+    auto lerp = [](double t, double a, double b) { return (1 - t) * a + t * b; };  // utility.h:84
+    double y0z0 = lerp(x, x000, x100), y1z0 = lerp(x, x010, x110), y0z1 = lerp(x, x001, x101),
+           y1z1 = lerp(x, x011, x111);
+    return lerp(z, lerp(y, y0z0, y1z0), lerp(y, y0z1, y1z1));
+  }
+  static v3 hash(const v3& u) {  // noise.h:141-145
+    v3 r(dot(u, v3(127.1, 311.7, 74.7)), dot(u, v3(269.5, 183.3, 246.1)), dot(u, v3(113.5, 271.9, 307.7)));
+    v3 q = v3(std::sin(r.x), std::sin(r.y), std::sin(r.z)) * 43758.5453;
+    return q - v3(std::floor(q.x), std::floor(q.y), std::floor(q.z));  // fract (vec3.h:87)
+  }
+  static double cells(const v3& p, bool voronoi) {  // noise.h:147-167, 178-200
+    v3 f(std::floor(p.x), std::floor(p.y), std::floor(p.z));
+    float min_dist = std::numeric_limits<float>::max(), color = 0.0f;
+    for (int i = -1; i <= 1; i++)
+      for (int j = -1; j <= 1; j++)
+        for (int k = -1; k <= 1; k++) {
+          v3 cell = f + v3(i, j, k);
+          v3 pos = cell + hash(cell);
+          float dist = (float)len(pos - p);
+          if (dist < min_dist) {
+            min_dist = dist;
+            if (voronoi) color = (float)hash(pos).x;
+          }
+        }
+    return voronoi ? color : min_dist * min_dist;
+  }
+};
+
 struct otex {
   int kind = RT_TEX_SOLID;
   v3 color, odd, even;
   double scale = 1;
+  onoise noise;
   v3 sample(double, double, const v3& p) const {
-    if (kind == RT_TEX_SOLID) return color;
-    v3 uv = p / scale;  // texture.h:48-55
-    int ix = (int)std::floor(uv.x);
-    int iy = (int)std::floor(uv.y);
-    int iz = (int)std::floor(uv.z);
-    int total = ix + iy + iz;
-    return (total % 2 == 0) ? even : odd;
+    switch (kind) {
+      case RT_TEX_SOLID: return color;
+      case RT_TEX_CHECKER: {
+        v3 uv = p / scale;  // texture.h:48-55
+        int ix = (int)std::floor(uv.x);
+        int iy = (int)std::floor(uv.y);
+        int iz = (int)std::floor(uv.z);
+        int total = ix + iy + iz;
+        return (total % 2 == 0) ? even : odd;
+      }
+      case RT_TEX_PERLIN: {  // texture.h:84-88
+        double g = .5 * (1 + std::sin((p.x + 70 * noise.turb(7, p / scale))));
+        return {g, g, g};
+      }
+      case RT_TEX_VALUE: {
+        double g = noise.value(p);
+        return {g, g, g};
+      }
+      default: {
+        double g = onoise::cells(p, kind == RT_TEX_VORONOI);
+        return {g, g, g};
+      }
+    }
   }
 };
 
@@ -1175,7 +1267,25 @@ void* orc_scene_from_desc(const rt_scene_desc* d, char* err, int errlen) {
       b.tex.push_back(s->solid(v3_from(t.color)));
     else if (t.kind == RT_TEX_CHECKER)
       b.tex.push_back(s->checker(v3_from(t.odd), v3_from(t.even), t.scale));
-    else
+    else if (t.kind >= RT_TEX_PERLIN && t.kind <= RT_TEX_VORONOI) {
+      auto tx = std::make_unique<otex>();
+      tx->kind = t.kind;
+      tx->scale = t.scale;
+      if (t.kind == RT_TEX_PERLIN) {
+        if (!d->tex_data || t.data < 0 || t.data + 6 * 256 > d->num_tex_data) return fail("perlin: tex_data too short");
+        const double* src = d->tex_data + t.data;
+        for (int k = 0; k < 256; k++) tx->noise.rand_offset.push_back(v3(src[3 * k], src[3 * k + 1], src[3 * k + 2]));
+        for (int k = 0; k < 256; k++) tx->noise.perm_x.push_back((int)src[768 + k]);
+      } else if (t.kind == RT_TEX_VALUE) {
+        int n = (int)t.scale;
+        if (n < 1 || !d->tex_data || t.data < 0 || t.data + (int64_t)n * n * n > d->num_tex_data)
+          return fail("value: bad resolution or tex_data too short");
+        tx->noise.resolution = n;
+        for (int64_t k = 0; k < (int64_t)n * n * n; k++) tx->noise.values.push_back((float)d->tex_data[t.data + k]);
+      }
+      s->texs.push_back(std::move(tx));
+      b.tex.push_back(s->texs.back().get());
+    } else
       return fail("unsupported texture kind");
   }
   for (int i = 0; i < d->num_materials; i++) {

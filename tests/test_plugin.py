@@ -64,3 +64,50 @@ def test_output_writers_match_the_reference_ppm(tmp_path):
     output.write_pfm(img.astype(np.float32), str(tmp_path / "a.pfm"))
     back = output.read_pfm(str(tmp_path / "a.pfm"))
     np.testing.assert_array_equal(np.nan_to_num(back, nan=-7), np.nan_to_num(img.astype(np.float32), nan=-7))
+
+
+NOISE_SCENES = ["test_perlin_noise", "test_value_noise", "test_worley_noise", "test_voronoi_noise",
+                "perlin_texture_ball"]
+
+
+@pytest.mark.parametrize("name", NOISE_SCENES)
+def test_noise_scenes_compile_and_render_on_the_oracle(name):
+    cs = plugin.ConfigScene(name, 24)
+    st, info, msg = abi.scene_check(cs.desc)
+    assert st == abi.RT_OK, msg
+    img, segs = oracle.render(oracle.from_desc(cs.desc), cs.cam, 2, 4, seed=2)
+    assert np.isfinite(img).all() and segs > 0 and img.max() > 0
+
+
+@pytest.mark.parametrize("kind", ["perlin", "value"])
+def test_python_noise_tables_match_the_plugin(kind):
+    # both draw from glibc rand() in the reference constructors' order (noise.h:12-20, 97-105)
+    import ctypes
+    from rt_amd.scene import SceneBuilder
+    libc = ctypes.CDLL(None)
+    name = {"perlin": "test_perlin_noise", "value": "test_value_noise"}[kind]
+    libc.srand(7)
+    cs = plugin.ConfigScene(name, 16)
+    tab = np.ctypeslib.as_array(cs.desc.tex_data, shape=(cs.desc.num_tex_data,)).copy()
+    libc.srand(7)
+    s = SceneBuilder()
+    s.perlin(1) if kind == "perlin" else s.value(40)
+    assert np.array_equal(tab, np.array(s.tex_data))
+    if kind == "perlin":  # 256 unit vectors, then three permutations of 0..255
+        assert np.allclose(np.linalg.norm(tab[:768].reshape(-1, 3), axis=1), 1)
+        for k in range(3):
+            assert sorted(tab[768 + 256 * k: 1024 + 256 * k]) == list(range(256))
+
+
+def test_bad_noise_tables_are_rejected():
+    from rt_amd.scene import SceneBuilder
+    s = SceneBuilder(rand=lambda: 0.25)
+    t = s.perlin(2)
+    s.tex_data = s.tex_data[:1000]  # too short
+    st, _, msg = abi.scene_check(s.desc(s.sphere((0, 0, 0), 1, s.lambertian(t))))
+    assert st != abi.RT_OK and "perlin" in msg
+    s2 = SceneBuilder(rand=lambda: 0.25)
+    t2 = s2.value(3)
+    s2.textures[t2].scale = 2.5  # not an integer resolution
+    st, _, msg = abi.scene_check(s2.desc(s2.sphere((0, 0, 0), 1, s2.lambertian(t2))))
+    assert st != abi.RT_OK and "value" in msg
