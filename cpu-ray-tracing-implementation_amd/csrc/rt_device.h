@@ -220,6 +220,7 @@ struct DevScene {
   int32_t has_volumes;
   uint32_t n_nodes;
   const double* texdata;  // procedural-texture tables (Texture::data)
+  const uint8_t* images;  // picture-texture pixels (Texture::data)
   int32_t has_procedural; // any perlin / value / worley / voronoi texture: the EXT kernels
 };
 
@@ -836,13 +837,32 @@ __device__ __forceinline__ double cell_noise(bool voronoi, double px, double py,
 
 // EXT: the kernel instantiation for scenes with procedural textures (or non-perspective
 // cameras); the base kernels only contain the solid and checker textures.
+// sphere::get_sphere_uv (sphere.h:90-95) of a unit vector
+template <class R>
+__device__ __forceinline__ void sphere_uv(V<R> n, double& u, double& v) {
+  const double theta = acos(-(double)n.y);
+  const double phi = atan2(-(double)n.z, (double)n.x) + 3.1415926535897932385;
+  u = phi / (2 * 3.1415926535897932385);
+  v = theta / 3.1415926535897932385;
+}
+
 template <class R, bool EXT>
-__device__ __forceinline__ V<R> tex_sample(const DevScene<R>& sc, const Texture<R>& tx, V<R> p) {  // texture.h
+__device__ __forceinline__ V<R> tex_sample(const DevScene<R>& sc, const Texture<R>& tx, V<R> p, double u = 0,
+                                           double v = 0) {  // texture.h
   if (!EXT || tx.kind == T_SOLID || tx.kind == T_CHECKER) {
     if (tx.kind == T_SOLID) return ld3(tx.c0);  // texture.h:15
     V<R> uv = p / tx.scale;                     // texture.h:47-56
     int total = (int)floor(uv.x) + (int)floor(uv.y) + (int)floor(uv.z);
     return (total % 2 == 0) ? ld3(tx.c1) : ld3(tx.c0);
+  }
+  if (tx.kind == T_IMAGE) {  // picture_texture::sample (texture.h:68-74), image::pixel_data (image.h:71-82)
+    const double cs = 1 / 256.0;
+    if (tx.n == 0 || tx.h == 0) return mkv(R(255 * cs), R(0), R(255 * cs));  // no image: magenta
+    int i = (int)(tx.n * u), j = (int)(tx.h * (1 - v));
+    i = i < 0 ? 0 : (i < (int)tx.n ? i : (int)tx.n - 1);  // clamp to [0, width)
+    j = j < 0 ? 0 : (j < (int)tx.h ? j : (int)tx.h - 1);
+    const uint8_t* px = sc.images + tx.data + 3 * ((size_t)j * tx.n + (size_t)i);
+    return mkv(R(px[0] * cs), R(px[1] * cs), R(px[2] * cs));
   }
   double g;
   if (tx.kind == T_PERLIN)

@@ -275,7 +275,9 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
     if (sc.background >= 0) {
       R tb;
       if (sphere_roots<R>(o.x, o.y, o.z, d.x, d.y, d.z, o.x, o.y, o.z, R(1), R(0.001), Num<R>::inf(), false, tb)) {
-        add = s.thr * tex_sample<R, CAMX>(sc, sc.texs[sc.background], o + tb * d);
+        double bu = 0, bv = 0;
+        if constexpr (CAMX) sphere_uv(tb * d, bu, bv);  // the unit sphere about the origin (camera.h:184-187)
+        add = s.thr * tex_sample<R, CAMX>(sc, sc.texs[sc.background], o + tb * d, bu, bv);
         has_add = true;
       }
     }
@@ -285,6 +287,7 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
     V<R> pw, n;
     bool front;
     int32_t mat;
+    double hu = 0, hv = 0;  // hit_record u, v (EXT kernels: picture textures); 0 where the reference leaves them stale
     if (ty == E_VOLUME) {  // volumne.h:40-44
       pw = o + t * d;
       n = mkv(R(1), R(0), R(0));
@@ -297,7 +300,7 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
       // fp32, planar primitives: instances are rigid, so the hit is o + t d in world space and
       // only the object-space normal needs rotating out (fp64 keeps the reference's
       // object-space point, hittable.h:75-82, 125-149)
-      const bool world_space = sizeof(R) == 4 && ty != E_SPHERE;
+      const bool world_space = sizeof(R) == 4 && ty != E_SPHERE && !CAMX;
       if (in && !world_space) chain_in(*in, oo, dd);
       V<R> po = oo + t * dd;
       V<R> outward;
@@ -305,6 +308,11 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
         const Quad<R>& q = sc.quads[idx];
         outward = ld3(q.n);
         mat = q.mat;
+        if constexpr (CAMX) {  // quad.h:47-62: u, v = alpha, beta
+          const V<R> rel = po - ld3(q.q);
+          hu = (double)dot(rel, ld3(q.a));
+          hv = (double)dot(rel, ld3(q.b));
+        }
       } else if (ty == E_SPHERE) {  // sphere.h:69 (center_ member; (0,0,0) for moving spheres)
         const Sphere<R>& sp = sc.spheres[idx];
         if constexpr (sizeof(R) == 8) {
@@ -329,6 +337,7 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
           outward = (po - ld3(sp.cn)) * fdiv(R(1), sp.r);
         }
         mat = sp.mat;
+        if constexpr (CAMX) sphere_uv(outward, hu, hv);  // sphere.h:70
       } else {
         const Tri<R>& tr = sc.tris[idx];
         outward = ld3(tr.n);
@@ -361,12 +370,12 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
     const Material<R>& m = sc.mats[mat];
     if (m.kind == M_DIFFUSE_LIGHT) {  // material.h:211-215; no scatter
       if (front) {
-        add = s.thr * tex_sample<R, CAMX>(sc, m.tx, pw);
+        add = s.thr * tex_sample<R, CAMX>(sc, m.tx, pw, hu, hv);
         has_add = true;
       }
       done = true;
     } else {
-      V<R> att = tex_sample<R, CAMX>(sc, m.tx, pw);
+      V<R> att = tex_sample<R, CAMX>(sc, m.tx, pw, hu, hv);
       const uint32_t bounce = (uint32_t)s.bounce;
       uint32_t js = 0;
       auto U = [&]() { return to_unit<R>(draw_u32(s.ks, dim_scatter(bounce, js++))); };
@@ -816,6 +825,7 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
   s.has_volumes = h.has_volumes;
   s.n_nodes = h.n_nodes;
   s.texdata = (const double*)at(h.off_texdata);
+  s.images = (const uint8_t*)at(h.off_images);
   s.has_procedural = h.n_texdata > 0 || h.has_cell_noise;
   return s;
 }

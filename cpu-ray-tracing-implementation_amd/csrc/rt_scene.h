@@ -143,7 +143,7 @@ struct alignas(16) Node {
 };
 
 enum : int32_t { M_LAMBERTIAN = 1, M_METAL = 2, M_DIELECTRIC = 3, M_ISOTROPIC = 4, M_DIFFUSE_LIGHT = 5, M_GLOSS = 6 };
-enum : int32_t { T_SOLID = 1, T_CHECKER = 2, T_PERLIN = 3, T_VALUE = 4, T_WORLEY = 5, T_VORONOI = 6 };
+enum : int32_t { T_SOLID = 1, T_CHECKER = 2, T_PERLIN = 3, T_VALUE = 4, T_WORLEY = 5, T_VORONOI = 6, T_IMAGE = 7 };
 constexpr uint32_t kPerlinPoints = 256;  // noise.h:76 point_count
 
 template <class R>
@@ -152,8 +152,10 @@ struct alignas(16) Texture {
   int32_t kind;
   R c1[3];  // checker even
   R scale;  // checker (texture.h:48), perlin (texture.h:87)
-  uint32_t data;  // perlin: rand_offset (256 x 3) then perm_x (256); value: n^3 values -- offsets into texdata
-  uint32_t n;     // value noise resolution
+  uint32_t data;  // perlin: rand_offset (256 x 3) then perm_x (256); value: n^3 values -- offsets into texdata;
+                  // image: byte offset into images
+  uint32_t n;     // value noise resolution; image width
+  uint32_t h;     // image height
 };
 // The material's texture is copied inline: shading reads one record per hit.
 template <class R>
@@ -194,8 +196,10 @@ struct SceneHeader {
       off_light, off_linear;  // off_linear: LinRec array
   uint64_t off_texdata;       // procedural-texture tables, double in both blobs (noise runs in fp64)
   uint64_t n_texdata;
-  int32_t has_cell_noise;     // a worley / voronoi texture (no tables)
+  int32_t has_cell_noise;     // a worley / voronoi / image texture (EXT kernels)
   int32_t pad2_;
+  uint64_t off_images;        // picture-texture pixels (RGB bytes)
+  uint64_t n_images;
   uint64_t bytes;
   uint32_t n_linear;  // 0: no linear program (use the BVH traversal)
   uint32_t pad_;

@@ -153,7 +153,8 @@ class Compiler {
   std::vector<uint32_t> refs_;
   std::vector<Material<double>> mats_;
   std::vector<double> texdata_;  // procedural-texture tables (Texture::data offsets)
-  bool cell_noise_ = false;      // a worley / voronoi texture
+  bool cell_noise_ = false;      // a worley / voronoi / image texture (EXT kernels)
+  std::vector<uint8_t> images_;  // picture-texture pixels
   std::vector<int32_t> mat_remap_;                    // descriptor material -> mats_ index
   std::unordered_map<std::string, int32_t> mat_index_;  // material record bytes -> mats_ index
   int32_t mat_id(int32_t m) const { return mat_remap_[(size_t)m]; }
@@ -696,6 +697,7 @@ Texture<float> to32(const Texture<double>& t) {
   r.scale = (float)t.scale;
   r.data = t.data;
   r.n = t.n;
+  r.h = t.h;
   return r;
 }
 Light<float> to32(const Light<double>& l) {
@@ -722,7 +724,8 @@ template <class Q, class S, class T, class I, class V, class N, class M, class X
 SceneHeader pack(std::vector<unsigned char>& blob, const std::vector<Q>& q, const std::vector<S>& s,
                  const std::vector<T>& t, const std::vector<I>& in, const std::vector<V>& vo, const std::vector<N>& nd,
                  const std::vector<uint32_t>& refs, const std::vector<M>& m, const std::vector<X>& x, const L& light,
-                 const std::vector<LR>& linear, const std::vector<double>& texdata) {
+                 const std::vector<LR>& linear, const std::vector<double>& texdata,
+                 const std::vector<uint8_t>& images) {
   SceneHeader h{};
   blob.clear();
   h.off_quads = append(blob, q);
@@ -739,6 +742,8 @@ SceneHeader pack(std::vector<unsigned char>& blob, const std::vector<Q>& q, cons
   h.n_linear = (uint32_t)linear.size();
   h.off_texdata = append(blob, texdata);
   h.n_texdata = texdata.size();
+  h.off_images = append(blob, images);
+  h.n_images = images.size();
   blob.resize((blob.size() + 255) & ~size_t(255));
   h.bytes = blob.size();
   h.n_quads = (uint32_t)q.size();
@@ -860,6 +865,19 @@ bool Compiler::run(CompiledScene* out, std::string* err) {
       r.n = (uint32_t)n;
       r.data = (uint32_t)texdata_.size();
       texdata_.insert(texdata_.end(), d_->tex_data + t.data, d_->tex_data + t.data + (int64_t)(n * n * n));
+    } else if (t.kind == RT_TEX_IMAGE) {  // texture.h:65-78: width x height RGB bytes
+      const double w = t.color[0], hh = t.color[1];
+      if (!(w >= 0 && hh >= 0 && w == (double)(int64_t)w && hh == (double)(int64_t)hh && w * hh <= 1e9) ||
+          (w * hh > 0 && (!d_->image_data || t.data < 0 || (int64_t)t.data + (int64_t)(w * hh * 3) > d_->num_image_data))) {
+        *err = "image texture " + std::to_string(i) + ": bad size or image_data too short";
+        return false;
+      }
+      r.kind = T_IMAGE;
+      r.n = (uint32_t)w;
+      r.h = (uint32_t)hh;
+      r.data = (uint32_t)images_.size();
+      if (w * hh > 0) images_.insert(images_.end(), d_->image_data + t.data, d_->image_data + t.data + (int64_t)(w * hh * 3));
+      cell_noise_ = true;  // EXT kernels
     } else if (t.kind == RT_TEX_WORLEY || t.kind == RT_TEX_VORONOI) {  // stateless (noise.h:139-201)
       r.kind = t.kind == RT_TEX_WORLEY ? T_WORLEY : T_VORONOI;
       cell_noise_ = true;
@@ -898,6 +916,7 @@ bool Compiler::run(CompiledScene* out, std::string* err) {
     put(&r.tx.scale, 8);
     put(&r.tx.data, 4);
     put(&r.tx.n, 4);
+    put(&r.tx.h, 4);
     auto it = mat_index_.find(key);
     if (it == mat_index_.end()) {
       it = mat_index_.emplace(key, (int32_t)mats_.size()).first;
@@ -940,9 +959,9 @@ bool Compiler::run(CompiledScene* out, std::string* err) {
   out->bvh_depth = root.depth;
   out->num_items = (int)top.size();
   out->hdr64 =
-      pack(out->blob64, quads_, spheres_, tris_, insts_, vols_, nodes_, refs_, mats_, texs_, light_, linear, texdata_);
+      pack(out->blob64, quads_, spheres_, tris_, insts_, vols_, nodes_, refs_, mats_, texs_, light_, linear, texdata_, images_);
   out->hdr = pack(out->blob32, map32(quads_), map32(spheres_), map32(tris_), map32(insts_), map32(vols_),
-                  map32(nodes_), refs_, map32(mats_), map32(texs_), to32(light_), map32(linear), texdata_);
+                  map32(nodes_), refs_, map32(mats_), map32(texs_), to32(light_), map32(linear), texdata_, images_);
   for (SceneHeader* h : {&out->hdr, &out->hdr64}) {
     h->has_cell_noise = cell_noise_ ? 1 : 0;
     h->root = root.entry;

@@ -22,7 +22,7 @@ RT_OBJ_SPHERE, RT_OBJ_QUAD, RT_OBJ_TRIANGLE, RT_OBJ_LIST, RT_OBJ_BVH, RT_OBJ_TRA
     RT_OBJ_ROTATE_Y, RT_OBJ_ROTATE_Z, RT_OBJ_VOLUME = range(1, 11)
 # rt_material_kind
 RT_MAT_LAMBERTIAN, RT_MAT_METAL, RT_MAT_DIELECTRIC, RT_MAT_ISOTROPIC, RT_MAT_DIFFUSE_LIGHT, RT_MAT_GLOSS = range(1, 7)
-RT_TEX_SOLID, RT_TEX_CHECKER, RT_TEX_PERLIN, RT_TEX_VALUE, RT_TEX_WORLEY, RT_TEX_VORONOI = range(1, 7)
+RT_TEX_SOLID, RT_TEX_CHECKER, RT_TEX_PERLIN, RT_TEX_VALUE, RT_TEX_WORLEY, RT_TEX_VORONOI, RT_TEX_IMAGE = range(1, 8)
 RT_CAM_PERSPECTIVE, RT_CAM_ORTHONORMAL, RT_CAM_FISHEYE, RT_CAM_LENS = range(4)
 RT_PREC_F32, RT_PREC_F64 = 0, 1
 ABI_VERSION = 2  # include/rt_hip.h RT_ABI_VERSION
@@ -49,7 +49,8 @@ class rt_scene_desc(ctypes.Structure):
                 ("materials", ctypes.POINTER(rt_material)), ("num_materials", c_int32),
                 ("textures", ctypes.POINTER(rt_texture)), ("num_textures", c_int32),
                 ("world", c_int32), ("light", c_int32), ("background", c_int32), ("pad_", c_int32),
-                ("tex_data", ctypes.POINTER(c_double)), ("num_tex_data", ctypes.c_int64)]
+                ("tex_data", ctypes.POINTER(c_double)), ("num_tex_data", ctypes.c_int64),
+                ("image_data", ctypes.POINTER(ctypes.c_uint8)), ("num_image_data", ctypes.c_int64)]
 
 
 class rt_camera_desc(ctypes.Structure):

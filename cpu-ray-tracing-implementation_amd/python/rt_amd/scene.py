@@ -5,6 +5,7 @@ Mirrors the constructors of the reference's hittables/materials/textures
 volumne.h, material.h, texture.h) so tests can build arbitrary scenes. The
 production caller is the C++ plugin surface in ../../rt/ (camera::render).
 """
+import ctypes
 import math
 
 import numpy as np
@@ -67,6 +68,19 @@ class SceneBuilder:
         rd = self._rand
         vals = [float(np.float32(rd())) for _ in range(resolution ** 3)]  # std::vector<float> (noise.h:135)
         t = abi.rt_texture(kind=abi.RT_TEX_VALUE, scale=float(resolution), data=self._emit_data(vals))
+        self.textures.append(t)
+        return len(self.textures) - 1
+
+    def image(self, linear_rgb):
+        """picture_texture (texture.h:65-78) over linear RGB floats (H, W, 3), row 0 at the top,
+        stored as bytes with image.h's float_to_byte. An empty array samples as magenta."""
+        a = np.asarray(linear_rgb, dtype=np.float32)
+        h, w = (a.shape[0], a.shape[1]) if a.size else (0, 0)
+        b = np.where(a <= 0, 0, np.where(a >= 1, 255, np.floor(256.0 * a.astype(np.float64)))).astype(np.uint8)
+        off = len(getattr(self, "image_data", b""))
+        self.image_data = getattr(self, "image_data", b"") + b.tobytes()
+        t = abi.rt_texture(kind=abi.RT_TEX_IMAGE, data=off)
+        t.color[0], t.color[1] = float(w), float(h)
         self.textures.append(t)
         return len(self.textures) - 1
 
@@ -168,9 +182,11 @@ class SceneBuilder:
             (abi.rt_material * max(1, len(self.materials)))(*self.materials),
             (abi.rt_texture * max(1, len(self.textures)))(*self.textures),
             (abi.c_double * max(1, len(self.tex_data)))(*self.tex_data),
+            (ctypes.c_uint8 * max(1, len(getattr(self, "image_data", b""))))(*getattr(self, "image_data", b"")),
         )
-        d.objects, d.children, d.materials, d.textures, d.tex_data = self._keep
+        d.objects, d.children, d.materials, d.textures, d.tex_data, d.image_data = self._keep
         d.num_tex_data = len(self.tex_data)
+        d.num_image_data = len(getattr(self, "image_data", b""))
         d.num_objects, d.num_children = len(self.objects), len(self.children)
         d.num_materials, d.num_textures = len(self.materials), len(self.textures)
         d.world, d.light, d.background = world, light, background

@@ -46,6 +46,12 @@ class scene_builder {
     textures_.push_back(t);
     return (int)textures_.size() - 1;
   }
+  // picture-texture pixels; returns their byte offset for rt_texture.data
+  int32_t emit_image_data(const std::vector<uint8_t>& v) {
+    const int32_t off = (int32_t)image_data_.size();
+    image_data_.insert(image_data_.end(), v.begin(), v.end());
+    return off;
+  }
   // procedural-texture tables; returns their offset for rt_texture.data
   int32_t emit_tex_data(const std::vector<double>& v) {
     const int32_t off = (int32_t)tex_data_.size();
@@ -68,6 +74,8 @@ class scene_builder {
     d.background = background;
     d.tex_data = tex_data_.empty() ? nullptr : tex_data_.data();
     d.num_tex_data = (int64_t)tex_data_.size();
+    d.image_data = image_data_.empty() ? nullptr : image_data_.data();
+    d.num_image_data = (int64_t)image_data_.size();
     return d;
   }
 
@@ -90,5 +98,6 @@ class scene_builder {
   std::vector<rt_material> materials_;
   std::vector<rt_texture> textures_;
   std::vector<double> tex_data_;
+  std::vector<uint8_t> image_data_;
   std::unordered_map<const void*, int> seen_obj_, seen_mat_, seen_tex_;
 };

@@ -5,6 +5,7 @@
 #include <memory>
 
 #include "color.h"
+#include "image.h"
 #include "noise.h"
 #include "ray.h"
 #include "scene_builder.h"
@@ -132,4 +133,28 @@ class voronoi_texture : public texture {  // texture.h:113-119
 
  private:
   voronoi_noise noise_;
+};
+
+// image colours at (u, v) (texture.h:65-78); u, v from the hit (sphere.h:90-95, quad.h:58-64)
+class picture_texture : public texture {
+ public:
+  explicit picture_texture(std::shared_ptr<image> img) : image_(std::move(img)) {}
+  color sample(double u, double v, point3) override {
+    int i = image_->width() * u;
+    int j = image_->height() * (1 - v);
+    const unsigned char* px = image_->pixel_data(i, j);
+    const double color_scale = 1 / 256.0;
+    return color(px[0] * color_scale, px[1] * color_scale, px[2] * color_scale);
+  }
+  int flatten(scene_builder& sb) const override {
+    rt_texture t{};
+    t.kind = RT_TEX_IMAGE;
+    t.color[0] = image_->width();
+    t.color[1] = image_->height();
+    if (image_->width() > 0) t.data = sb.emit_image_data(image_->bytes());
+    return sb.emit_texture(t);
+  }
+
+ private:
+  std::shared_ptr<image> image_;
 };

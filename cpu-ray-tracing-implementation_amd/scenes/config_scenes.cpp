@@ -179,6 +179,31 @@ void perlin_texture_ball(int width, double aspect, config_scene* s) {  // main.c
   // cam.render(of, bvh): the light is not importance-sampled in this scene (main.cc:436)
 }
 
+// The reference's asset directory (./assets); $RT_ASSETS overrides it.
+std::string asset(const std::string& name) {
+  const char* dir = std::getenv("RT_ASSETS");
+  return std::string(dir && *dir ? dir : "./assets") + "/" + name;
+}
+
+void skybox_and_fisheye(int width, double aspect, config_scene* s) {  // main.cc:173-183
+  auto skybox = std::make_shared<picture_texture>(std::make_shared<image>(asset("bathroom.exr").c_str()));
+  auto world = std::make_shared<hittable_list>();
+  world->push_back(std::make_shared<sphere>(vec3(0), 1, std::make_shared<dielectric>(solid_color::white, 1.0)));
+  s->world = world;
+  s->cam.initialize_fisheye(W(width, 600), A(aspect, 1), point3(1.1, 1.8, 1.1), point3(0, 0, 0), 1.0, 90, 500, 5);
+  s->cam.background_ = skybox;
+}
+
+void skybox_and_motion_blur(int width, double aspect, config_scene* s) {  // main.cc:185-196
+  auto skybox = std::make_shared<picture_texture>(std::make_shared<image>(asset("bathroom.exr").c_str()));
+  auto world = std::make_shared<hittable_list>();
+  auto earth_tex = std::make_shared<picture_texture>(std::make_shared<image>(asset("earthmap.jpg").c_str()));
+  world->push_back(std::make_shared<sphere>(vec3(-0.2, 0, 0), vec3(0.2, 0, 0), 1, std::make_shared<lambertian>(earth_tex)));
+  s->world = world;
+  s->cam.initialize_perspective(W(width, 600), A(aspect, 1), point3(0, 0, 4), point3(0, 0, 0), 1.0, 70, 500, 5);
+  s->cam.background_ = skybox;
+}
+
 // main.cc:447-485: the triangles sponza() builds from the loader's output primitives -- float
 // positions only, uint16 indices only (other index types leave the primitive empty), and
 // consecutive position triples when a primitive has no indices.
@@ -249,6 +274,10 @@ bool build_config_scene(const std::string& name, int width, double aspect, confi
     three_material_ball_with_defocus_blur(width, aspect, out);
   else if (name == "sponza")
     sponza(width, aspect, out);
+  else if (name == "skybox_and_fisheye")
+    skybox_and_fisheye(width, aspect, out);
+  else if (name == "skybox_and_motion_blur")
+    skybox_and_motion_blur(width, aspect, out);
   else if (name == "perlin_texture_ball")
     perlin_texture_ball(width, aspect, out);
   else if (name == "test_perlin_noise")

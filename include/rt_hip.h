@@ -106,12 +106,16 @@ typedef enum rt_texture_kind {
                          then perm_x, perm_y, perm_z (256 each) as the constructor drew them */
   RT_TEX_VALUE = 4,   /* texture.h:95-103, noise.h:95-137. scale = resolution n; tex_data[data ..]: n^3 values */
   RT_TEX_WORLEY = 5,  /* texture.h:105-111, noise.h:139-168 */
-  RT_TEX_VORONOI = 6  /* texture.h:113-119, noise.h:170-201 */
+  RT_TEX_VORONOI = 6, /* texture.h:113-119, noise.h:170-201 */
+  RT_TEX_IMAGE = 7    /* texture.h:65-78, image.h: color[0] = width, color[1] = height; the pixels are
+                         width * height * 3 bytes (row 0 at the top, RGB) at image_data[data]. A 0 x 0
+                         image samples as magenta, like a file the reference could not load. */
 } rt_texture_kind;
 
 typedef struct rt_texture {
   int32_t kind;
-  int32_t data;    /* perlin / value: offset of the texture's tables in rt_scene_desc.tex_data */
+  int32_t data;    /* perlin / value: offset of the texture's tables in rt_scene_desc.tex_data;
+                      image: byte offset of its pixels in rt_scene_desc.image_data */
   double color[3]; /* solid */
   double odd[3];   /* checker */
   double even[3];  /* checker */
@@ -133,6 +137,8 @@ typedef struct rt_scene_desc {
   int32_t pad_;
   const double* tex_data; /* procedural-texture tables (rt_texture.data), may be NULL */
   int64_t num_tex_data;
+  const uint8_t* image_data; /* picture-texture pixels (rt_texture.data), may be NULL */
+  int64_t num_image_data;
 } rt_scene_desc;
 
 /* ---- camera: the values camera::initialize_* computes (camera.h:21-132) ---- */

@@ -274,8 +274,20 @@ struct otex {
   v3 color, odd, even;
   double scale = 1;
   onoise noise;
-  v3 sample(double, double, const v3& p) const {
+  int width = 0, height = 0;   // image
+  std::vector<uint8_t> pixels;  // image, RGB rows from the top (image.h bdata)
+  v3 sample(double u, double v, const v3& p) const {
     switch (kind) {
+      case RT_TEX_IMAGE: {  // picture_texture::sample (texture.h:68-74), image::pixel_data (image.h:71-82)
+        double cs = 1 / 256.0;
+        if (width == 0 || height == 0) return v3(255 * cs, 0, 255 * cs);  // magenta: no image data
+        int i = width * u;
+        int j = height * (1 - v);
+        i = i < 0 ? 0 : (i < width ? i : width - 1);
+        j = j < 0 ? 0 : (j < height ? j : height - 1);
+        const uint8_t* px = pixels.data() + 3 * ((size_t)j * width + i);
+        return v3(px[0] * cs, px[1] * cs, px[2] * cs);
+      }
       case RT_TEX_SOLID: return color;
       case RT_TEX_CHECKER: {
         v3 uv = p / scale;  // texture.h:48-55
@@ -580,6 +592,7 @@ struct otri : ohit {  // triangle.h
     if (b0 < 0 || b1 < 0 || b0 + b1 > 1) return false;
     rec.t = th;
     rec.p = r.at(th);
+    rec.u = rec.v = 0;  // the reference leaves u, v stale (triangle.h:27-40); the device uses 0 too
     rec.set_face_normal(r, normal);
     rec.mat = mat;
     return true;
@@ -732,6 +745,7 @@ struct ovolume : ohit {  // volumne.h
     rec.t = r1.t + hd / rl;
     rec.p = r.at(rec.t);
     rec.n = v3(1, 0, 0);
+    rec.u = rec.v = 0;  // stale in the reference (volumne.h:40-44); 0 here and on the device
     rec.front = true;
     rec.mat = phase;
     return true;
@@ -1267,7 +1281,17 @@ void* orc_scene_from_desc(const rt_scene_desc* d, char* err, int errlen) {
       b.tex.push_back(s->solid(v3_from(t.color)));
     else if (t.kind == RT_TEX_CHECKER)
       b.tex.push_back(s->checker(v3_from(t.odd), v3_from(t.even), t.scale));
-    else if (t.kind >= RT_TEX_PERLIN && t.kind <= RT_TEX_VORONOI) {
+    else if (t.kind == RT_TEX_IMAGE) {
+      auto tx = std::make_unique<otex>();
+      tx->kind = RT_TEX_IMAGE;
+      tx->width = (int)t.color[0];
+      tx->height = (int)t.color[1];
+      const int64_t n = 3LL * tx->width * tx->height;
+      if (n > 0 && (!d->image_data || t.data < 0 || t.data + n > d->num_image_data)) return fail("image: data too short");
+      if (n > 0) tx->pixels.assign(d->image_data + t.data, d->image_data + t.data + n);
+      s->texs.push_back(std::move(tx));
+      b.tex.push_back(s->texs.back().get());
+    } else if (t.kind >= RT_TEX_PERLIN && t.kind <= RT_TEX_VORONOI) {
       auto tx = std::make_unique<otex>();
       tx->kind = t.kind;
       tx->scale = t.scale;

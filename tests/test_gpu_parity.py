@@ -252,6 +252,36 @@ def test_noise_textures_match_oracle(ctx, name):
         assert (rmse(img32, ref) < 1e-3).all(), rmse(img32, ref)
 
 
+@pytest.mark.parametrize("name", ["skybox_and_fisheye", "skybox_and_motion_blur"])
+def test_picture_textures_match_oracle(ctx, name, tmp_path, monkeypatch):
+    # texture.h:65-78 + image.h: sphere uv (sphere.h:90-95), background uv of the unit sphere about
+    # the ray origin (camera.h:180-190), fisheye camera; assets written as PFM / PPM
+    from test_plugin import _write_assets
+    _write_assets(tmp_path)
+    monkeypatch.setenv("RT_ASSETS", str(tmp_path))
+    cs = plugin.ConfigScene(name, 40)
+    img, ref, _ = render_both(ctx, cs.desc, cs.cam, 4, 5, 3, F64)
+    assert np.all(np.abs(img - ref) <= 1e-9 * np.maximum(1.0, np.abs(ref))), np.abs(img - ref).max()
+    img32, _, _ = render_both(ctx, cs.desc, cs.cam, 4, 5, 3, F32)
+    np.testing.assert_allclose(img32.reshape(-1, 3).mean(0), ref.reshape(-1, 3).mean(0), rtol=1e-2)
+
+
+def test_picture_texture_on_quads_matches_oracle(ctx):
+    # quad uv = (alpha, beta) (quad.h:58-64), inside a rotated instance, plus a textured sphere
+    s = SceneBuilder()
+    tex = s.image(np.random.default_rng(4).uniform(0, 1, (9, 13, 3)))
+    lam = s.lambertian(tex)
+    light = s.diffuse_light(s.solid((6, 6, 6)))
+    lq = s.quad((-1, 3, -1), (2, 0, 0), (0, 0, 2), light)
+    objs = [s.quad((-3, 0, -3), (6, 0, 0), (0, 0, 6), lam),
+            s.rotate(1, s.quad((-1, 0.5, 0), (2, 0, 0), (0, 2, 0), lam), 30),
+            s.sphere((1.5, 1, 1), 0.7, lam), lq]
+    cam = perspective(40, 1.0, (0, 2, 6), (0, 1, 0), 1, 50.0)
+    desc = s.desc(s.hlist(objs), light=lq, background=s.solid((0.1, 0.1, 0.1)))
+    img, ref, _ = render_both(ctx, desc, cam, 4, 5, 2, F64)
+    assert np.all(np.abs(img - ref) <= 1e-9 * np.maximum(1.0, np.abs(ref))), np.abs(img - ref).max()
+
+
 def test_full_c2_fp32_matches_fp64(ctx):
     # BASELINE config 2 at full size: the fp32 production path against the fp64 device path
     cs = plugin.ConfigScene("cornell_box", 800)

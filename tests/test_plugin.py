@@ -111,3 +111,37 @@ def test_bad_noise_tables_are_rejected():
     s2.textures[t2].scale = 2.5  # not an integer resolution
     st, _, msg = abi.scene_check(s2.desc(s2.sphere((0, 0, 0), 1, s2.lambertian(t2))))
     assert st != abi.RT_OK and "value" in msg
+
+
+def _write_assets(d):
+    from rt_amd import output
+    sky = np.random.default_rng(1).uniform(-0.1, 1.2, (24, 48, 3)).astype(np.float32)
+    output.write_pfm(sky, str(d / "bathroom.exr"))  # the loader reads the header, not the extension
+    earth = np.random.default_rng(2).integers(0, 256, (12, 20, 3), dtype=np.uint8)
+    (d / "earthmap.jpg").write_bytes(b"P6\n# comment\n20 12\n255\n" + earth.tobytes())
+    return sky, earth
+
+
+def test_picture_texture_bytes(tmp_path, monkeypatch):
+    # image.h: linear floats -> float_to_byte (<= 0 -> 0, >= 1 -> 255, else int(256 v)); 8-bit files
+    # come back linear as (b / 255)^2.2 (stbi_loadf)
+    sky, earth = _write_assets(tmp_path)
+    monkeypatch.setenv("RT_ASSETS", str(tmp_path))
+    cs = plugin.ConfigScene("skybox_and_motion_blur", 16)
+    data = np.ctypeslib.as_array(cs.desc.image_data, shape=(cs.desc.num_image_data,))
+    to_byte = lambda f: np.where(f <= 0, 0, np.where(f >= 1, 255, np.floor(256.0 * f))).astype(np.uint8)
+    sky_b = to_byte(sky.astype(np.float64)).ravel()
+    earth_b = to_byte(np.power(earth / 255.0, 2.2).astype(np.float32).astype(np.float64)).ravel()
+    assert data.size == sky_b.size + earth_b.size
+    texs = [cs.desc.textures[i] for i in range(cs.desc.num_textures) if cs.desc.textures[i].kind == abi.RT_TEX_IMAGE]
+    by_size = {int(t.color[0] * t.color[1] * 3): t.data for t in texs}
+    off_sky, off_earth = by_size[sky_b.size], by_size[earth_b.size]
+    assert np.array_equal(data[off_sky:off_sky + sky_b.size], sky_b)
+    assert np.array_equal(data[off_earth:off_earth + earth_b.size], earth_b)
+
+
+def test_missing_image_samples_magenta(monkeypatch, tmp_path):
+    monkeypatch.setenv("RT_ASSETS", str(tmp_path / "none"))
+    cs = plugin.ConfigScene("skybox_and_motion_blur", 8)
+    img, _ = oracle.render(oracle.from_desc(cs.desc), cs.cam, 1, 3, seed=1)
+    assert np.allclose(img[..., 1], 0) and np.allclose(img[..., 0], img[..., 2]) and img.max() > 0.9
