@@ -7,7 +7,7 @@ ARCH     ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC -Wall --offload-arch=$(ARCH)
 
 LIB_SRCS := $(PKG)/csrc/rt_kernels.hip $(PKG)/csrc/scene_compile.cpp
-LIB_HDRS := $(PKG)/csrc/rt_device.h $(PKG)/csrc/rt_scene.h $(PKG)/csrc/scene_compile.h include/rt_hip.h
+LIB_HDRS := $(PKG)/csrc/rt_device.h $(PKG)/csrc/rt_sin.h $(PKG)/csrc/rt_scene.h $(PKG)/csrc/scene_compile.h include/rt_hip.h
 
 CXX      ?= g++
 CXXFLAGS ?= -O2 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter

@@ -8,6 +8,7 @@
 #include <stdint.h>
 
 #include "rt_scene.h"
+#include "rt_sin.h"
 
 namespace rtd {
 
@@ -803,7 +804,8 @@ __device__ __forceinline__ void cell_hash(double ux, double uy, double uz, doubl
   const double ax = ux * 127.1 + uy * 311.7 + uz * 74.7;
   const double ay = ux * 269.5 + uy * 183.3 + uz * 246.1;
   const double az = ux * 113.5 + uy * 271.9 + uz * 307.7;
-  const double sx = sin(ax) * 43758.5453, sy = sin(ay) * 43758.5453, sz = sin(az) * 43758.5453;
+  // correctly rounded sin (rt_sin.h): the hash is chaotic in sin's last bit
+  const double sx = sin_cr(ax) * 43758.5453, sy = sin_cr(ay) * 43758.5453, sz = sin_cr(az) * 43758.5453;
   hx = sx - floor(sx);
   hy = sy - floor(sy);
   hz = sz - floor(sz);

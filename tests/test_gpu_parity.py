@@ -238,10 +238,12 @@ def test_noise_textures_match_oracle(ctx, name):
     img, ref, _ = render_both(ctx, cs.desc, cs.cam, 4, 5, 8, F64)
     bad = np.abs(img - ref) > 1e-9 * np.maximum(1.0, np.abs(ref))
     if name == "test_voronoi_noise":
-        # voronoi hashes the feature point itself: fract(43758.5 sin(~2e4)) turns the last-ulp
-        # difference between the device's and glibc's sin into a different value for a rare
-        # sample (the other noises match to 1e-9)
-        assert bad.any(-1).mean() < 0.01 and (rmse(img, ref) < 1e-4).all(), rmse(img, ref)
+        # voronoi hashes the feature point itself: fract(43758.5 sin(~2e4)) turns a last-ulp
+        # difference in sin into a different colour. The device's sin is correctly rounded
+        # (rt_sin.h); glibc's is in all but ~0.15 % of arguments, which leaves a rare cell apart
+        # (the other noises match to 1e-9). Measured: 1.4 % of pixels (one or two cells), RMSE 1e-6;
+        # the libm sin instead gave 15 % and 9e-6
+        assert bad.any(-1).mean() < 0.03 and (rmse(img, ref) < 1e-5).all(), rmse(img, ref)
     else:
         assert not bad.any(), np.abs(img - ref).max()
     img32, _, _ = render_both(ctx, cs.desc, cs.cam, 4, 5, 8, F32)
