@@ -90,7 +90,7 @@ def measured_traffic(workload):
 
 def workload_key(scene_name, W, H, spp, depth, args):
     return (f"{scene_name} {W}x{H} {spp}spp depth {depth} {args.precision} pool={args.pool} chunk={args.chunk} "
-            f"K={args.segments_per_launch} world={args.gpus}")
+            f"K={args.segments_per_launch} world={args.gpus}" + (" ordered" if args.traversal == "ordered" else ""))
 
 
 def main():
@@ -104,6 +104,8 @@ def main():
     ap.add_argument("--chunk", type=int, default=0, help="samples per work item (0 = library default)")
     ap.add_argument("--segments-per-launch", type=int, default=0,
                     help="segments each path slot advances per k_step launch (0 = library default)")
+    ap.add_argument("--traversal", default="auto", choices=["auto", "ordered"],
+                    help="ordered: the reference-ordered linear program / BVH also in fp32 (no flat program)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--kernel-timing", default="on", choices=["on", "off"],
                     help="HIP events around every extend/shade launch of the timed steps (roofline)")
@@ -136,7 +138,8 @@ def main():
     my_tiles = all_tiles[rank]
     out = torch.zeros((maxpix, 3), dtype=tdtype, device=dev)
     params = ctx.params(spp, depth, args.seed, prec, samples_per_item=args.chunk, pool_slots=args.pool,
-                        segments_per_launch=args.segments_per_launch)
+                        segments_per_launch=args.segments_per_launch,
+                        traversal=abi.RT_TRAV_ORDERED if args.traversal == "ordered" else abi.RT_TRAV_AUTO)
     fb = gathered = scatter_idx = None
     if rank == 0:
         fb = torch.zeros((H * W, 3), dtype=tdtype, device=dev)

@@ -216,6 +216,10 @@ struct DevScene {
   const Light<R>* light;
   const LinRec<R>* lin;  // linear program (n_linear > 0)
   uint32_t n_linear;
+  const FlatQuad* flatq;  // flat program (fp32, has_flat): quads grouped by plane axis, then boxes
+  const FlatBox* flatb;
+  uint32_t n_flatq[3], n_flatb;
+  int32_t has_flat;
   uint32_t root;
   int32_t background;
   int32_t has_volumes;
@@ -738,6 +742,114 @@ __device__ __forceinline__ void trace_linear(const DevScene<R>& sc, V<R> wo, V<R
     }
   }
   t_best = tmax;
+}
+
+// ------------------------------------------------------------------ flat program (fp32)
+// rt_scene.h FlatQuad / FlatBox: world-space axis-aligned quads in three branch-free loops
+// (one per plane axis, records scalar-loaded in pairs), then the slab tests of the boxes.
+// A quad is the aquad_t test (quad.h:30-64 for n = +-e_A); the record index of the closest
+// hit is kept and turned into (entry, instance) once at the end.
+struct FlatQuad2 {
+  FlatQuad a, b;
+};
+template <int A>
+__device__ __forceinline__ void flat_quad_test(const FlatQuad& r, int32_t idx, V<float> o, V<float> d,
+                                               V<float> inv, float tmin, float& tmax, int32_t& best,
+                                               uint64_t xkey) {
+  constexpr int U = A == 0 ? 1 : 0, W = A == 2 ? 1 : 2;
+  const float th = (r.plane - comp<A>(o)) * comp<A>(inv);
+  const float a = ((comp<U>(o) + th * comp<U>(d)) - r.lo_u) * r.inv_u;
+  const float b = ((comp<W>(o) + th * comp<W>(d)) - r.lo_w) * r.inv_w;
+  const uint32_t lo = __float_as_uint(tmin);
+  const bool in_t = __float_as_uint(th) - lo <= __float_as_uint(tmax) - lo;
+  const bool in_ab = max(__float_as_uint(a), __float_as_uint(b)) <= 0x3f800000u;
+  const uint64_t key = ((uint64_t)(uint32_t)r.inst << 32) | r.e;
+  const bool h = in_t & in_ab & (key != xkey);
+  tmax = h ? th : tmax;
+  best = h ? idx : best;
+}
+template <int A>
+__device__ __forceinline__ void flat_quads(const FlatQuad* q, uint32_t n, int32_t base, V<float> o, V<float> d,
+                                           V<float> inv, float tmin, float& tmax, int32_t& best, uint64_t xkey) {
+  const FlatQuad2* q2 = reinterpret_cast<const FlatQuad2*>(q);
+#pragma unroll 1
+  for (uint32_t k = 0; k < n; k += 2) {
+    const FlatQuad2 r = ld_uniform(q2, k >> 1);
+    flat_quad_test<A>(r.a, base + (int32_t)k, o, d, inv, tmin, tmax, best, xkey);
+    flat_quad_test<A>(r.b, base + (int32_t)k + 1, o, d, inv, tmin, tmax, best, xkey);
+  }
+}
+// Slab test of a box (= the closest of its six quads): entry distance tn, or the exit tf for
+// a ray that starts inside (what the quads give). A ray leaving one of the box's faces
+// (excl_i == inst; the face is excl_e & 7, rt_scene.h) starts on that face's plane: its
+// distance to it becomes -inf, i.e. the plane is behind the ray whichever way it goes --
+// a ray going out then has tf < 0 (no hit), one going in exits through another face.
+struct Slab {
+  float t0[3], t1[3], tn, tf, th;
+};
+__device__ __forceinline__ Slab flat_slab(const FlatBox& b, V<float> o, V<float> inv, float tmin, int32_t excl_i,
+                                          uint32_t xf) {
+  Slab s;
+  const bool left = excl_i == b.inst;
+  const float ninf = -Num<float>::inf();
+  s.t0[0] = (left & (xf == 0)) ? ninf : (b.lo[0] - o.x) * inv.x;
+  s.t1[0] = (left & (xf == 1)) ? ninf : (b.hi[0] - o.x) * inv.x;
+  s.t0[1] = (left & (xf == 2)) ? ninf : (b.lo[1] - o.y) * inv.y;
+  s.t1[1] = (left & (xf == 3)) ? ninf : (b.hi[1] - o.y) * inv.y;
+  s.t0[2] = (left & (xf == 4)) ? ninf : (b.lo[2] - o.z) * inv.z;
+  s.t1[2] = (left & (xf == 5)) ? ninf : (b.hi[2] - o.z) * inv.z;
+  s.tn = fmaxf(fmaxf(fminf(s.t0[0], s.t1[0]), fminf(s.t0[1], s.t1[1])), fminf(s.t0[2], s.t1[2]));
+  s.tf = fminf(fminf(fmaxf(s.t0[0], s.t1[0]), fmaxf(s.t0[1], s.t1[1])), fmaxf(s.t0[2], s.t1[2]));
+  s.th = s.tn >= tmin ? s.tn : s.tf;
+  return s;
+}
+__device__ __forceinline__ void trace_flat(const DevScene<float>& sc, V<float> o, V<float> d, uint32_t excl_e,
+                                           int32_t excl_i, float& t_best, uint32_t& e_best, int32_t& i_best) {
+  const float tmin = 0.001f;
+  float tmax = Num<float>::inf();
+  const V<float> inv = rcp3(d);
+  const uint64_t xkey = ((uint64_t)(uint32_t)excl_i << 32) | excl_e;
+  const uint32_t xf = excl_e & 7u;
+  int32_t best = -1;
+  const uint32_t n0 = sc.n_flatq[0], n1 = sc.n_flatq[1], n2 = sc.n_flatq[2], nq = n0 + n1 + n2;
+  flat_quads<0>(sc.flatq, n0, 0, o, d, inv, tmin, tmax, best, xkey);
+  flat_quads<1>(sc.flatq + n0, n1, (int32_t)n0, o, d, inv, tmin, tmax, best, xkey);
+  flat_quads<2>(sc.flatq + n0 + n1, n2, (int32_t)(n0 + n1), o, d, inv, tmin, tmax, best, xkey);
+#pragma unroll 1
+  for (uint32_t k = 0; k < sc.n_flatb; k++) {
+    const FlatBox b = ld_uniform(sc.flatb, k);
+    const Slab s = flat_slab(b, o, inv, tmin, excl_i, xf);
+    const bool h = (s.tn <= s.tf) & (s.th >= tmin) & (s.th <= tmax);
+    tmax = h ? s.th : tmax;
+    best = h ? (int32_t)(nq + k) : best;
+  }
+  t_best = tmax;
+  e_best = kNoHit;
+  i_best = -1;
+  if (best < 0) return;
+  if ((uint32_t)best < nq) {
+    const FlatQuad& r = sc.flatq[best];
+    e_best = r.e;
+    i_best = r.inst;
+    return;
+  }
+  // the face of the box: the axis whose slab bound is the hit distance (recomputed exactly
+  // as in the loop), on the side the ray enters (or leaves, from inside)
+  const FlatBox& b = sc.flatb[(uint32_t)best - nq];
+  const Slab s = flat_slab(b, o, inv, tmin, excl_i, xf);
+  const bool enter = s.tn >= tmin;
+  int k = 2;
+  if (enter) {
+    if (s.tn == fminf(s.t0[0], s.t1[0])) k = 0;
+    else if (s.tn == fminf(s.t0[1], s.t1[1])) k = 1;
+  } else {
+    if (s.tf == fmaxf(s.t0[0], s.t1[0])) k = 0;
+    else if (s.tf == fmaxf(s.t0[1], s.t1[1])) k = 1;
+  }
+  const float dk = k == 0 ? d.x : (k == 1 ? d.y : d.z);
+  const int side = enter ? (dk < 0.f ? 1 : 0) : (dk < 0.f ? 0 : 1);
+  e_best = b.face[2 * k + side];
+  i_best = b.inst;
 }
 
 // ------------------------------------------------------------------ textures, pdfs

@@ -496,6 +496,19 @@ struct LinearTrav {
     trace_linear<R, SPH, TRI, VOL>(sc, s.o, s.d, s.tm, s.xe, s.xi, k, (uint32_t)s.bounce, t, e, i);
   }
 };
+// The flat program (fp32, quad/box scenes such as every Cornell config): rt_device.h trace_flat.
+#ifndef RT_FLAT_WAVES
+#define RT_FLAT_WAVES 6
+#endif
+struct FlatTrav {
+  static constexpr int kStack = 0;
+  static constexpr int kWaves = RT_FLAT_WAVES;
+  static constexpr int kLdsNodes = 0;
+  __device__ __forceinline__ static void run(const DevScene<float>& sc, const Node<float>*, const Path<float>& s,
+                                             Keys, uint32_t*, float& t, uint32_t& e, int32_t& i) {
+    trace_flat(sc, s.o, s.d, s.xe, s.xi, t, e, i);
+  }
+};
 // LDSN: the scene's BVH nodes (at most kLdsNodeMax) are copied into LDS at kernel start, so
 // every traversal step reads LDS instead of waiting on the memory hierarchy (RTOW: 117 nodes)
 constexpr uint32_t kLdsNodeMax = 256;
@@ -820,6 +833,11 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
   s.light = (const Light<R>*)at(h.off_light);
   s.lin = (const LinRec<R>*)at(h.off_linear);
   s.n_linear = h.n_linear;
+  s.has_flat = (int32_t)h.has_flat;
+  s.flatq = (const FlatQuad*)at(h.off_flat_quad);
+  s.flatb = (const FlatBox*)at(h.off_flat_box);
+  for (int a = 0; a < 3; a++) s.n_flatq[a] = h.n_flat_quad[a];
+  s.n_flatb = h.n_flat_box;
   s.root = h.root;
   s.background = h.background;
   s.has_volumes = h.has_volumes;
@@ -845,6 +863,13 @@ void launch_k(const Params<R>& p, uint32_t grid, hipStream_t st) {
 template <class R>
 void launch_step(const Params<R>& p, int stack, bool sph, bool tri, uint32_t grid, hipStream_t st) {
   const bool vol = p.sc.has_volumes != 0;
+  if constexpr (sizeof(R) == 4) {
+    // the flat program (world-space quads and boxes); the extended kernels keep the linear one
+    if (p.sc.has_flat && p.cam_mode == RT_CAM_PERSPECTIVE && !p.sc.has_procedural) {
+      hipLaunchKernelGGL((k_step_occ<float, FlatTrav, false>), dim3(grid), dim3(kBlock), 0, st, p);
+      return;
+    }
+  }
   if (p.sc.n_linear > 0) {
     if (!sph && !tri && !vol)
       launch_k<R, LinearTrav<R, false, false, false>>(p, grid, st);
@@ -921,6 +946,7 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     unsigned char* sp = (unsigned char*)c->state.ptr;
     Params<R> p{};
     p.sc = dev_scene<R>(hdr, sbase);
+    if (prm->traversal == RT_TRAV_ORDERED) p.sc.has_flat = 0;
     std::memcpy(&p.light, (f64 ? cs.blob64 : cs.blob32).data() + hdr.off_light, sizeof(Light<R>));
     p.O = (R4<R>*)sp;
     p.D = (R4<R>*)(sp + r4);
@@ -1123,7 +1149,9 @@ rt_status rt_scene_check(const rt_scene_desc* desc, rt_scene_info* info, char* e
   if (err && errlen > 0) std::snprintf(err, (size_t)errlen, "%s", m.c_str());
   if (s == RT_OK && info) {
     const SceneHeader& h = cs.hdr;
-    info->quads = (int32_t)h.n_quads;
+    info->quads = cs.desc_quads;
+    info->flat_quads = cs.flat_quads;
+    info->flat_boxes = cs.flat_boxes;
     info->spheres = (int32_t)h.n_spheres;
     info->triangles = (int32_t)h.n_tris;
     info->instances = h.num_instances;

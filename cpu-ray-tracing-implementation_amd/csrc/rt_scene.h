@@ -68,6 +68,36 @@ struct alignas(16) LinRec {
 };
 static_assert(3 * kMaxChain <= 14, "an instance chain must fit one LinRec");
 
+// The *flat program* (fp32 kernels only): a linear program whose ops are all axis-aligned
+// quads, at world level or under translate-only instances, is rewritten in world space
+// (translations folded into the records) and regrouped by plane axis, so a wave runs three
+// branch-free loops with no per-op dispatch. An instance holding exactly the six quads of
+// `box()` (quad.h:91-112) with one lambertian material becomes one slab-test record. Order
+// inside the scene only decides exact-t ties, which fp32 does not reproduce anyway; the fp64
+// path keeps the reference-ordered linear program.
+//   FlatQuad, group A (plane axis): U < W are the two other axes,
+//     alpha = (o_U + t d_U - lo_u) * inv_u, beta = (o_W + t d_W - lo_w) * inv_w (signed inv);
+//   groups are padded to an even count with records whose plane is NaN (never hit).
+struct alignas(16) FlatQuad {
+  float plane, lo_u, lo_w, inv_u;
+  float inv_w;
+  uint32_t e;    // the quad's entry (shade reads its normal and material)
+  int32_t inst;  // its instance (translate-only), -1 at world level
+  uint32_t pad;
+};
+//   FlatBox: the slab [lo, hi]; face[2k + s] is the entry of the face on plane lo_k (s = 0)
+//   or hi_k (s = 1). A ray leaving any of its faces excludes the whole box: the faces are
+//   lambertian, so a continuing ray leaves the convex box outward (a light sample below the
+//   surface has p_scattered = 0 and ends the path).
+struct alignas(16) FlatBox {
+  float lo[3];
+  int32_t inst;
+  float hi[3];
+  uint32_t pad;
+  uint32_t face[6];
+  uint32_t pad2[2];
+};
+
 // quad.h:9-23 precomputed: n = unit(cross(u,v)), D = dot(n, corner),
 // a = cross(v, w), b = cross(w, u) with w = cross(u,v)/dot(cross(u,v),cross(u,v)),
 // so alpha = dot(p - corner, a) = dot(w, cross(p - corner, v)) and beta = dot(p - corner, b).
@@ -202,7 +232,10 @@ struct SceneHeader {
   uint64_t n_images;
   uint64_t bytes;
   uint32_t n_linear;  // 0: no linear program (use the BVH traversal)
-  uint32_t pad_;
+  uint32_t n_flat_box;          // flat program (fp32 blob only): boxes
+  uint32_t n_flat_quad[3];      // flat program: quads per plane axis (even counts)
+  uint32_t has_flat;            // 1: the flat program replaces the linear program in fp32
+  uint64_t off_flat_quad, off_flat_box;
   uint32_t n_quads, n_spheres, n_tris, n_volumes, n_nodes, n_refs, n_mats, n_texs;
 };
 

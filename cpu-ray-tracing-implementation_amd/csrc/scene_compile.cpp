@@ -191,6 +191,8 @@ class Compiler {
   Item bvh(std::vector<Item>& items, size_t b, size_t e, int depth);
   int make_instance(const std::vector<Op>& chain, uint32_t blas);
   LinRec<double> lin_record(uint32_t op) const;
+  bool flat_program(const std::vector<uint32_t>& lin, std::vector<FlatQuad>& quads, uint32_t nq[3],
+                    std::vector<FlatBox>& boxes);
   std::vector<int> aligned_;  // per quad: 1 + perm for axis-aligned quads, 0 otherwise
   std::vector<double> qu_, qv_;  // per quad: u[U], v[V] (aligned quads)
   void light_from(int idx);
@@ -816,6 +818,148 @@ LinRec<double> Compiler::lin_record(uint32_t op) const {
   return r;
 }
 
+// The flat program of rt_scene.h (fp32 kernels): the linear program's ops are all
+// axis-aligned quads, at world level or in translate-only instances. Returns false (no flat
+// program) for anything else.
+bool Compiler::flat_program(const std::vector<uint32_t>& lin, std::vector<FlatQuad>& quads, uint32_t nq[3],
+                            std::vector<FlatBox>& boxes) {
+  struct Q {
+    uint32_t e;
+    int32_t inst;
+    int A, U, W;        // plane axis; U < W the other two
+    double plane, lo_u, lo_w, len_u, len_w;  // object space
+  };
+  auto quad_of = [&](uint32_t op, int32_t inst, Q& q) {
+    const uint32_t i = epay(op);
+    if (etype(op) != E_QUAD || !aligned_[i]) return false;
+    const int* ax = kPermAxes[aligned_[i] - 1];  // A, axis of u, axis of v
+    q.e = op;
+    q.inst = inst;
+    q.A = ax[0];
+    q.plane = quads_[i].q[ax[0]];
+    double lu = quads_[i].q[ax[1]], lv = quads_[i].q[ax[2]], su = qu_[i], sv = qv_[i];
+    if (ax[1] < ax[2]) {
+      q.U = ax[1], q.W = ax[2], q.lo_u = lu, q.lo_w = lv, q.len_u = su, q.len_w = sv;
+    } else {
+      q.U = ax[2], q.W = ax[1], q.lo_u = lv, q.lo_w = lu, q.len_u = sv, q.len_w = su;
+    }
+    return true;
+  };
+  std::vector<FlatQuad> grp[3];
+  auto add_quad = [&](const Q& q, const double* off) {
+    FlatQuad r{};
+    r.plane = (float)(q.plane + off[q.A]);
+    r.lo_u = (float)(q.lo_u + off[q.U]);
+    r.lo_w = (float)(q.lo_w + off[q.W]);
+    r.inv_u = (float)(1.0 / q.len_u);
+    r.inv_w = (float)(1.0 / q.len_w);
+    r.e = q.e;
+    r.inst = q.inst;
+    grp[q.A].push_back(r);
+  };
+  // six quads of box() (quad.h:91-112) with one lambertian material -> one slab record
+  auto as_box = [&](const std::vector<Q>& qs, const double* off, FlatBox& b) {  // b.face: original entries
+    if (qs.size() != 6) return false;
+    const int32_t mat = quads_[epay(qs[0].e)].mat;
+    if (mats_[(size_t)mat].kind != M_LAMBERTIAN) return false;
+    double lo[3], hi[3];
+    int cnt[3] = {0, 0, 0};
+    for (const Q& q : qs) {
+      if (quads_[epay(q.e)].mat != mat) return false;
+      if (cnt[q.A] == 0) lo[q.A] = hi[q.A] = q.plane;
+      lo[q.A] = std::min(lo[q.A], q.plane);
+      hi[q.A] = std::max(hi[q.A], q.plane);
+      cnt[q.A]++;
+    }
+    for (int k = 0; k < 3; k++)
+      if (cnt[k] != 2 || !(lo[k] < hi[k])) return false;
+    int seen[6] = {0, 0, 0, 0, 0, 0};
+    for (const Q& q : qs) {  // each face spans the box exactly in its two in-plane axes
+      const double u0 = std::min(q.lo_u, q.lo_u + q.len_u), u1 = std::max(q.lo_u, q.lo_u + q.len_u);
+      const double w0 = std::min(q.lo_w, q.lo_w + q.len_w), w1 = std::max(q.lo_w, q.lo_w + q.len_w);
+      if (u0 != lo[q.U] || u1 != hi[q.U] || w0 != lo[q.W] || w1 != hi[q.W]) return false;
+      const int f = 2 * q.A + (q.plane == hi[q.A] ? 1 : 0);
+      if (seen[f]++) return false;
+      b.face[f] = q.e;
+    }
+    for (int k = 0; k < 3; k++) {
+      b.lo[k] = (float)(lo[k] + off[k]);
+      b.hi[k] = (float)(hi[k] + off[k]);
+    }
+    b.inst = qs[0].inst;
+    return true;
+  };
+  const double zero[3] = {0, 0, 0};
+  const size_t quads_before = quads_.size();
+  auto undo = [&]() {
+    quads_.resize(quads_before);
+    aligned_.resize(quads_before);
+    qu_.resize(quads_before);
+    qv_.resize(quads_before);
+    return false;
+  };
+  for (size_t k = 0; k < lin.size(); k++) {
+    const uint32_t op = lin[k];
+    if (etype(op) == E_QUAD) {
+      Q q;
+      if (!quad_of(op, -1, q)) return undo();
+      add_quad(q, zero);
+      continue;
+    }
+    if (etype(op) != E_INSTANCE) return undo();
+    const int32_t ii = (int32_t)epay(op);
+    const Instance<double>& in = insts_[(size_t)ii];
+    double off[3] = {0, 0, 0};
+    for (int j = 0; j < in.nops; j++) {
+      if (in.op[j].kind != 0) return undo();  // rotations: the linear program
+      off[0] += in.op[j].x;
+      off[1] += in.op[j].y;
+      off[2] += in.op[j].z;
+    }
+    std::vector<Q> qs;
+    for (k++; k < lin.size() && lin[k] != kInstEnd; k++) {
+      Q q;
+      if (!quad_of(lin[k], ii, q)) return undo();
+      qs.push_back(q);
+    }
+    if (k == lin.size()) return undo();
+    FlatBox b{};
+    if (as_box(qs, off, b)) {
+      // the faces get copies of their quad records at an 8-aligned index, face j at base + j:
+      // a ray leaving the box knows from its entry which slab plane it starts on (trace_flat)
+      while (quads_.size() % 8) {
+        quads_.push_back(quads_[0]);
+        aligned_.push_back(aligned_[0]);
+        qu_.push_back(qu_[0]);
+        qv_.push_back(qv_[0]);
+      }
+      for (int f = 0; f < 6; f++) {
+        const uint32_t i = epay(b.face[f]);
+        quads_.push_back(quads_[i]);
+        aligned_.push_back(aligned_[i]);
+        qu_.push_back(qu_[i]);
+        qv_.push_back(qv_[i]);
+        b.face[f] = mk(E_QUAD, (uint32_t)quads_.size() - 1);
+      }
+      boxes.push_back(b);
+    } else
+      for (const Q& q : qs) add_quad(q, off);
+  }
+  quads.clear();
+  for (int a = 0; a < 3; a++) {
+    if (grp[a].size() % 2) {  // pad to pairs: a NaN plane never hits
+      FlatQuad pad{};
+      pad.plane = std::numeric_limits<float>::quiet_NaN();
+      pad.e = kNoHit;
+      pad.inst = -2;
+      grp[a].push_back(pad);
+    }
+    nq[a] = (uint32_t)grp[a].size();
+    quads.insert(quads.end(), grp[a].begin(), grp[a].end());
+  }
+  return true;
+}
+
 bool Compiler::run(CompiledScene* out, std::string* err) {
   if (!d_) {
     *err = "null scene descriptor";
@@ -955,6 +1099,16 @@ bool Compiler::run(CompiledScene* out, std::string* err) {
   std::vector<LinRec<double>> linear;
   if (lin_top.lin_ok)
     for (uint32_t op : lin_top.lin) linear.push_back(lin_record(op));
+  // the flat program of the fp32 blob, when the linear program has that form (may add quad records)
+  std::vector<FlatQuad> fq;
+  std::vector<FlatBox> fb;
+  uint32_t nq[3] = {0, 0, 0};
+  out->desc_quads = (int)quads_.size();
+  const bool has_flat = lin_top.lin_ok && !lin_top.lin.empty() && flat_program(lin_top.lin, fq, nq, fb);
+  if (has_flat) {
+    for (const FlatQuad& q : fq) out->flat_quads += q.inst != -2;
+    out->flat_boxes = (int)fb.size();
+  }
   out->stack_need = std::max(1, root.need);
   out->bvh_depth = root.depth;
   out->num_items = (int)top.size();
@@ -962,6 +1116,15 @@ bool Compiler::run(CompiledScene* out, std::string* err) {
       pack(out->blob64, quads_, spheres_, tris_, insts_, vols_, nodes_, refs_, mats_, texs_, light_, linear, texdata_, images_);
   out->hdr = pack(out->blob32, map32(quads_), map32(spheres_), map32(tris_), map32(insts_), map32(vols_),
                   map32(nodes_), refs_, map32(mats_), map32(texs_), to32(light_), map32(linear), texdata_, images_);
+  if (has_flat) {
+    out->hdr.off_flat_quad = append(out->blob32, fq);
+    out->hdr.off_flat_box = append(out->blob32, fb);
+    out->blob32.resize((out->blob32.size() + 255) & ~size_t(255));
+    out->hdr.bytes = out->blob32.size();
+    for (int a = 0; a < 3; a++) out->hdr.n_flat_quad[a] = nq[a];
+    out->hdr.n_flat_box = (uint32_t)fb.size();
+    out->hdr.has_flat = 1;
+  }
   for (SceneHeader* h : {&out->hdr, &out->hdr64}) {
     h->has_cell_noise = cell_noise_ ? 1 : 0;
     h->root = root.entry;

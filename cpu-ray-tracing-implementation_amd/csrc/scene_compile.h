@@ -20,6 +20,8 @@ struct CompiledScene {
   int stack_need = 0;  // traversal stack entries a lane can need
   int bvh_depth = 0;
   int num_items = 0;
+  int desc_quads = 0;  // quads of the descriptor (the flat program adds face copies)
+  int flat_quads = 0, flat_boxes = 0;
 };
 
 // Returns RT_OK or an error with a message.

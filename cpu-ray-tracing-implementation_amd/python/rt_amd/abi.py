@@ -25,7 +25,8 @@ RT_MAT_LAMBERTIAN, RT_MAT_METAL, RT_MAT_DIELECTRIC, RT_MAT_ISOTROPIC, RT_MAT_DIF
 RT_TEX_SOLID, RT_TEX_CHECKER, RT_TEX_PERLIN, RT_TEX_VALUE, RT_TEX_WORLEY, RT_TEX_VORONOI, RT_TEX_IMAGE = range(1, 8)
 RT_CAM_PERSPECTIVE, RT_CAM_ORTHONORMAL, RT_CAM_FISHEYE, RT_CAM_LENS = range(4)
 RT_PREC_F32, RT_PREC_F64 = 0, 1
-ABI_VERSION = 2  # include/rt_hip.h RT_ABI_VERSION
+RT_TRAV_AUTO, RT_TRAV_ORDERED = 0, 1
+ABI_VERSION = 3  # include/rt_hip.h RT_ABI_VERSION
 
 
 class rt_object(ctypes.Structure):
@@ -63,7 +64,7 @@ class rt_camera_desc(ctypes.Structure):
 class rt_render_params(ctypes.Structure):
     _fields_ = [("spp", c_int32), ("max_depth", c_int32), ("seed", c_uint64), ("precision", c_int32),
                 ("first_sample", c_int32), ("samples_per_item", c_int32), ("pool_slots", c_int32),
-                ("segments_per_launch", c_int32), ("pad_", c_int32)]
+                ("segments_per_launch", c_int32), ("traversal", c_int32)]
 
 
 class rt_tile(ctypes.Structure):
@@ -78,7 +79,7 @@ class rt_counters(ctypes.Structure):
 class rt_scene_info(ctypes.Structure):
     _fields_ = [("quads", c_int32), ("spheres", c_int32), ("triangles", c_int32), ("instances", c_int32),
                 ("volumes", c_int32), ("bvh_nodes", c_int32), ("linear_ops", c_int32), ("stack_need", c_int32),
-                ("bytes_f32", c_uint64), ("bytes_f64", c_uint64)]
+                ("bytes_f32", c_uint64), ("bytes_f64", c_uint64), ("flat_quads", c_int32), ("flat_boxes", c_int32)]
 
 
 # every symbol include/rt_hip.h declares, with its ctypes signature

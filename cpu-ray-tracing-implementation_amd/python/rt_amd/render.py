@@ -46,10 +46,11 @@ class Context:
 
     @staticmethod
     def params(spp, max_depth, seed=1, precision=abi.RT_PREC_F32, first_sample=0, samples_per_item=0, pool_slots=0,
-               segments_per_launch=0):
+               segments_per_launch=0, traversal=0):
         return abi.rt_render_params(spp=spp, max_depth=max_depth, seed=seed, precision=precision,
                                     first_sample=first_sample, samples_per_item=samples_per_item,
-                                    pool_slots=pool_slots, segments_per_launch=segments_per_launch)
+                                    pool_slots=pool_slots, segments_per_launch=segments_per_launch,
+                                    traversal=traversal)
 
     def render_tiles(self, cam, params, tiles, out_ptr, out_is_device, stream=None):
         arr = (abi.rt_tile * max(1, len(tiles)))(*[abi.rt_tile(*t) for t in tiles])

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 typedef enum rt_status {
   RT_OK = 0,
@@ -182,8 +182,15 @@ typedef struct rt_render_params {
   int32_t pool_slots;       /* wavefront pool size (0 = auto). Does not change the image. */
   int32_t segments_per_launch; /* segments each path slot advances per kernel launch (0 = auto).
                                   Does not change the image. */
-  int32_t pad_;
+  int32_t traversal;        /* rt_traversal: 0 = auto. RT_TRAV_ORDERED keeps the reference-ordered
+                               linear program / BVH in fp32 too (the fp32 flat program of quad/box
+                               scenes differs from it only in exact-t ties and rounding). */
 } rt_render_params;
+
+typedef enum rt_traversal {
+  RT_TRAV_AUTO = 0,
+  RT_TRAV_ORDERED = 1
+} rt_traversal;
 
 /* A framebuffer rectangle. Output of a render call is the tiles packed in the
  * given order, each row-major (top row first, camera.h:170), 3 channels per
@@ -214,6 +221,8 @@ typedef struct rt_scene_info {
   int32_t stack_need; /* traversal stack entries a ray can need (BVH path) */
   uint64_t bytes_f32; /* device scene size, fp32 / fp64 paths */
   uint64_t bytes_f64;
+  int32_t flat_quads; /* fp32 flat program (quad/box scenes): world-space axis-aligned quads */
+  int32_t flat_boxes; /*   and lambertian boxes traced as one slab test each; 0/0 = none */
 } rt_scene_info;
 
 typedef struct rt_context rt_context;

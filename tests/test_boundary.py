@@ -28,7 +28,7 @@ def test_every_declared_symbol_is_exported():
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(abi.SIGNATURES), set(names) ^ set(abi.SIGNATURES)
-    assert lib.rt_abi_version() == abi.ABI_VERSION == 2
+    assert lib.rt_abi_version() == abi.ABI_VERSION == 3
 
 
 def test_struct_layout_matches_c(tmp_path):
@@ -54,15 +54,18 @@ def test_context_create_without_device_fails_cleanly():
     assert b"device" in lib.rt_last_error(None)
 
 
-@pytest.mark.parametrize("name,quads,spheres,linear", [("cornell_box", 18, 0, True),
-                                                       ("cornell_box_with_volume", 18, 0, True),
-                                                       ("three_material_ball", 0, 4, True), ("rtow", 0, 339, False)])
-def test_scene_check_config_scenes(name, quads, spheres, linear):
+@pytest.mark.parametrize("name,quads,spheres,linear,flat", [("cornell_box", 18, 0, True, (6, 2)),
+                                                            ("cornell_box_with_volume", 18, 0, True, (0, 0)),
+                                                            ("three_material_ball", 0, 4, True, (0, 0)),
+                                                            ("rtow", 0, 339, False, (0, 0))])
+def test_scene_check_config_scenes(name, quads, spheres, linear, flat):
     desc, _, _, _ = scenes.SCENES[name](width=16)
     st, info, msg = abi.scene_check(desc)
     assert st == abi.RT_OK, msg
     assert (info.quads, info.spheres) == (quads, spheres)
     assert (info.linear_ops > 0) == linear
+    # fp32 flat program: Cornell's 5 walls + light as world-space quads, its 2 translated boxes as slabs
+    assert (info.flat_quads, info.flat_boxes) == flat
     if not linear:
         assert info.bvh_nodes > 0 and 1 <= info.stack_need <= 32
 
