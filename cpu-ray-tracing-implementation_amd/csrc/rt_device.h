@@ -804,7 +804,8 @@ __device__ __forceinline__ Slab flat_slab(const FlatBox& b, V<float> o, V<float>
   return s;
 }
 __device__ __forceinline__ void trace_flat(const DevScene<float>& sc, V<float> o, V<float> d, uint32_t excl_e,
-                                           int32_t excl_i, float& t_best, uint32_t& e_best, int32_t& i_best) {
+                                           int32_t excl_i, float& t_best, uint32_t& e_best, int32_t& i_best,
+                                           uint32_t& nm) {
   const float tmin = 0.001f;
   float tmax = Num<float>::inf();
   const V<float> inv = rcp3(d);
@@ -826,11 +827,13 @@ __device__ __forceinline__ void trace_flat(const DevScene<float>& sc, V<float> o
   t_best = tmax;
   e_best = kNoHit;
   i_best = -1;
+  nm = 0;
   if (best < 0) return;
   if ((uint32_t)best < nq) {
     const FlatQuad& r = sc.flatq[best];
     e_best = r.e;
     i_best = r.inst;
+    nm = r.nm;
     return;
   }
   // the face of the box: the axis whose slab bound is the hit distance (recomputed exactly
@@ -850,6 +853,7 @@ __device__ __forceinline__ void trace_flat(const DevScene<float>& sc, V<float> o
   const int side = enter ? (dk < 0.f ? 1 : 0) : (dk < 0.f ? 0 : 1);
   e_best = b.face[2 * k + side];
   i_best = b.inst;
+  nm = b.mat | (uint32_t)k << 28 | ((b.neg >> (2 * k + side)) & 1u) << 31;
 }
 
 // ------------------------------------------------------------------ textures, pdfs

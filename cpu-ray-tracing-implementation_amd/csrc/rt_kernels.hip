@@ -94,10 +94,12 @@ struct Params {
   uint4* S;
   uint4* X;
   R* partial;              // per item: 3 sums
-  const uint32_t* pixmap;  // local pixel -> global pixel id y*W + x
+  const uint32_t* pixmap;  // local pixel -> its image position x | y << 16
   const uint32_t* queue;   // live slots, or null = slots [0, n)
   uint32_t n;
   uint32_t P, npix, n_items, chunk, spp, first_sample, W;
+  uint64_t npix_m;  // item / npix = (item * npix_m) >> npix_k for every item < 2^31 (div_magic)
+  uint32_t npix_k;
   int32_t max_depth;
   uint64_t seed;
   // camera rays are built in fp64 for both paths (fp32 rounds once): the perspective camera
@@ -158,13 +160,13 @@ __device__ __forceinline__ void store_path(const Params<R>& p, uint32_t slot, co
 // A new work item for the slot: its pixel and that pixel's RNG key.
 template <class R>
 __device__ __forceinline__ void begin_item(const Params<R>& p, Path<R>& s, uint32_t item) {
-  const uint32_t chunk = item / p.npix;
-  const uint32_t gpix = p.pixmap[item - chunk * p.npix];
+  const uint32_t chunk = (uint32_t)(((uint64_t)item * p.npix_m) >> p.npix_k);
+  const uint32_t xy = p.pixmap[item - chunk * p.npix];
   s.item = item;
   s.sample = chunk * p.chunk;
   s.send = min(s.sample + p.chunk, p.spp);
-  s.xy = (gpix % p.W) | ((gpix / p.W) << 16);
-  s.ka = key_pixel(p.seed, gpix);
+  s.xy = xy;
+  s.ka = key_pixel(p.seed, (xy >> 16) * p.W + (xy & 0xFFFFu));
 }
 
 // camera::generate_ray for the orthonormal, fisheye and lens models (camera.h:252-290), reading
@@ -259,8 +261,10 @@ __global__ __launch_bounds__(kBlock) void k_init(Params<R> p) {
 // closest hit (t, e, inst) of s's ray, add emission, scatter (or finish the
 // sample and regenerate the slot's next camera ray). Returns false once the slot
 // has no work left.
-template <class R, bool CAMX>
-__device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t inst) {
+// FLAT: the hit comes from the flat program (trace_flat): a quad whose outward normal (+-e_A)
+// and material are packed in nm, so no primitive or instance record is read.
+template <class R, bool CAMX, bool FLAT = false>
+__device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t inst, uint32_t nm = 0) {
   const DevScene<R>& sc = p.sc;
   V<R> add = mkv(R(0), R(0), R(0));
   bool has_add = false, done = false;
@@ -288,7 +292,15 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
     bool front;
     int32_t mat;
     double hu = 0, hv = 0;  // hit_record u, v (EXT kernels: picture textures); 0 where the reference leaves them stale
-    if (ty == E_VOLUME) {  // volumne.h:40-44
+    if constexpr (FLAT) {  // quad.h:47-50 with n = +-e_A (translate leaves it alone, hittable.h:75-82)
+      const uint32_t A = (nm >> 28) & 3u;
+      const R sg = (nm >> 31) ? R(-1) : R(1);
+      const V<R> outward = mkv(A == 0 ? sg : R(0), A == 1 ? sg : R(0), A == 2 ? sg : R(0));
+      mat = (int32_t)(nm & kNmMat);
+      pw = o + t * d;
+      front = dot(d, outward) < R(0);  // hit_record::set_face_normal (hittable.h:26-29)
+      n = front ? outward : -outward;
+    } else if (ty == E_VOLUME) {  // volumne.h:40-44
       pw = o + t * d;
       n = mkv(R(1), R(0), R(0));
       front = true;
@@ -491,8 +503,9 @@ struct LinearTrav {
   // lean quad-only program fits 96 VGPRs with a small spill, the others would spill heavily
   static constexpr int kWaves = (sizeof(R) == 4 && !SPH && !TRI && !VOL) ? RT_LINEAR_WAVES : 1;
   static constexpr int kLdsNodes = 0;
+  static constexpr bool kFlat = false;
   __device__ __forceinline__ static void run(const DevScene<R>& sc, const Node<R>*, const Path<R>& s, Keys k,
-                                             uint32_t*, R& t, uint32_t& e, int32_t& i) {
+                                             uint32_t*, R& t, uint32_t& e, int32_t& i, uint32_t&) {
     trace_linear<R, SPH, TRI, VOL>(sc, s.o, s.d, s.tm, s.xe, s.xi, k, (uint32_t)s.bounce, t, e, i);
   }
 };
@@ -504,9 +517,10 @@ struct FlatTrav {
   static constexpr int kStack = 0;
   static constexpr int kWaves = RT_FLAT_WAVES;
   static constexpr int kLdsNodes = 0;
+  static constexpr bool kFlat = true;
   __device__ __forceinline__ static void run(const DevScene<float>& sc, const Node<float>*, const Path<float>& s,
-                                             Keys, uint32_t*, float& t, uint32_t& e, int32_t& i) {
-    trace_flat(sc, s.o, s.d, s.xe, s.xi, t, e, i);
+                                             Keys, uint32_t*, float& t, uint32_t& e, int32_t& i, uint32_t& nm) {
+    trace_flat(sc, s.o, s.d, s.xe, s.xi, t, e, i, nm);
   }
 };
 // LDSN: the scene's BVH nodes (at most kLdsNodeMax) are copied into LDS at kernel start, so
@@ -517,8 +531,9 @@ struct StackTrav {
   static constexpr int kStack = STACK;
   static constexpr int kLdsNodes = LDSN ? (int)kLdsNodeMax : 0;
   static constexpr int kWaves = sizeof(R) == 4 ? RT_STACK_WAVES : 1;  // fp32: occupancy over a small spill
+  static constexpr bool kFlat = false;
   __device__ __forceinline__ static void run(const DevScene<R>& sc, const Node<R>* nodes, const Path<R>& s, Keys k,
-                                             uint32_t* stk, R& t, uint32_t& e, int32_t& i) {
+                                             uint32_t* stk, R& t, uint32_t& e, int32_t& i, uint32_t&) {
     trace<R, STACK, kBlock>(sc, LDSN ? nodes : sc.nodes, s.o, s.d, s.tm, s.xe, s.xi, k, (uint32_t)s.bounce, stk,
                             t, e, i);
   }
@@ -564,22 +579,22 @@ __device__ __forceinline__ void step_body(const Params<R>& p) {
 #pragma unroll 1
     for (int k = 0; k < p.K; k++) {
       R t;
-      uint32_t e;
+      uint32_t e, nm = 0;
       int32_t inst;
 #ifdef RT_SECTION_CLOCKS
       const uint64_t c0 = clock64();
 #endif
-      Trav::run(p.sc, lds_nodes, s, Keys{s.ks}, stk.v + threadIdx.x, t, e, inst);
+      Trav::run(p.sc, lds_nodes, s, Keys{s.ks}, stk.v + threadIdx.x, t, e, inst, nm);
       segs++;
 #ifdef RT_SECTION_CLOCKS
       const uint64_t c1 = clock64();
-      const bool more = shade<R, CAMX>(p, s, t, e, inst);
+      const bool more = shade<R, CAMX, Trav::kFlat>(p, s, t, e, inst, nm);
       const uint64_t c2 = clock64();
       c_trace += c1 - c0;
       c_shade += c2 - c1;
       if (!more) break;
 #else
-      if (!shade<R, CAMX>(p, s, t, e, inst)) break;
+      if (!shade<R, CAMX, Trav::kFlat>(p, s, t, e, inst, nm)) break;
 #endif
     }
 #ifdef RT_SECTION_CLOCKS
@@ -817,6 +832,16 @@ hipEvent_t take_event(rt_context* c, size_t idx) {
   return c->events[idx];
 }
 
+// Division by a launch constant d >= 1 as a multiply (Granlund-Montgomery): with
+// k = 32 + ceil(log2 d) and m = floor(2^k / d) + 1, (n * m) >> k == n / d for every n < 2^31
+// (m d - 2^k <= d, so the error n (m d - 2^k) / 2^k stays below 1/d; n m < 2^64).
+void div_magic(uint32_t d, uint64_t& m, uint32_t& k) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) l++;
+  k = 32 + l;
+  m = (uint64_t)((((unsigned __int128)1) << k) / d) + 1;
+}
+
 template <class R>
 DevScene<R> dev_scene(const SceneHeader& h, void* base) {
   auto at = [&](uint64_t off) { return (const unsigned char*)base + off; };
@@ -905,7 +930,7 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
   for (int t = 0; t < ntiles; t++)
     for (int y = 0; y < tiles[t].height; y++)
       for (int x = 0; x < tiles[t].width; x++)
-        pix.push_back((uint32_t)(tiles[t].y0 + y) * (uint32_t)cam->image_width + (uint32_t)(tiles[t].x0 + x));
+        pix.push_back((uint32_t)(tiles[t].x0 + x) | (uint32_t)(tiles[t].y0 + y) << 16);
   const uint32_t npix = (uint32_t)pix.size();
   if (npix == 0) return RT_OK;
   const size_t out_elems = 3ull * npix;
@@ -961,6 +986,7 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     p.n = P;
     p.P = P;
     p.npix = npix;
+    div_magic(npix, p.npix_m, p.npix_k);
     p.n_items = n_items;
     p.chunk = chunk;
     p.spp = spp;
@@ -1174,6 +1200,8 @@ rt_status rt_render_tiles(rt_context* c, const rt_camera_desc* cam, const rt_ren
   if (cam->mode < RT_CAM_PERSPECTIVE || cam->mode > RT_CAM_LENS)
     return set_err(c, RT_ERR_INVALID_ARGUMENT, "unknown camera mode");
   if (cam->image_width <= 0 || cam->image_height <= 0) return set_err(c, RT_ERR_INVALID_ARGUMENT, "empty image");
+  if (cam->image_width > 65535 || cam->image_height > 65535)  // pixel positions are packed x | y << 16
+    return set_err(c, RT_ERR_INVALID_ARGUMENT, "image wider or taller than 65535 pixels");
   if (prm->spp <= 0) return set_err(c, RT_ERR_INVALID_ARGUMENT, "spp must be positive");
   if (prm->precision != RT_PREC_F32 && prm->precision != RT_PREC_F64)
     return set_err(c, RT_ERR_INVALID_ARGUMENT, "unknown precision");

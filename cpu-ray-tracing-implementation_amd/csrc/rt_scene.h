@@ -78,24 +78,27 @@ static_assert(3 * kMaxChain <= 14, "an instance chain must fit one LinRec");
 //   FlatQuad, group A (plane axis): U < W are the two other axes,
 //     alpha = (o_U + t d_U - lo_u) * inv_u, beta = (o_W + t d_W - lo_w) * inv_w (signed inv);
 //   groups are padded to an even count with records whose plane is NaN (never hit).
+//   nm (both records) = what shade needs of the hit: material | A << 28 | (n_A < 0) << 31, the
+//   quad's outward normal being +-e_A exactly (translations leave normals alone).
 struct alignas(16) FlatQuad {
   float plane, lo_u, lo_w, inv_u;
   float inv_w;
-  uint32_t e;    // the quad's entry (shade reads its normal and material)
+  uint32_t e;    // the quad's entry (exclusion state; its record is not read again)
   int32_t inst;  // its instance (translate-only), -1 at world level
-  uint32_t pad;
+  uint32_t nm;
 };
+constexpr uint32_t kNmMat = (1u << 28) - 1u;
 //   FlatBox: the slab [lo, hi]; face[2k + s] is the entry of the face on plane lo_k (s = 0)
-//   or hi_k (s = 1). A ray leaving any of its faces excludes the whole box: the faces are
-//   lambertian, so a continuing ray leaves the convex box outward (a light sample below the
-//   surface has p_scattered = 0 and ends the path).
+//   or hi_k (s = 1); the compiler gives the faces quad records at an 8-aligned index, face f
+//   at base + f, so a ray leaving the box knows the plane it starts on (trace_flat).
 struct alignas(16) FlatBox {
   float lo[3];
   int32_t inst;
   float hi[3];
-  uint32_t pad;
+  uint32_t mat;
   uint32_t face[6];
-  uint32_t pad2[2];
+  uint32_t neg;  // bit f: face f's outward normal points to -e_k
+  uint32_t pad;
 };
 
 // quad.h:9-23 precomputed: n = unit(cross(u,v)), D = dot(n, corner),

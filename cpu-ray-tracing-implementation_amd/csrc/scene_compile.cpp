@@ -855,6 +855,8 @@ bool Compiler::flat_program(const std::vector<uint32_t>& lin, std::vector<FlatQu
     r.inv_w = (float)(1.0 / q.len_w);
     r.e = q.e;
     r.inst = q.inst;
+    const Quad<double>& qq = quads_[epay(q.e)];
+    r.nm = (uint32_t)qq.mat | (uint32_t)q.A << 28 | (qq.n[q.A] < 0 ? 1u << 31 : 0u);
     grp[q.A].push_back(r);
   };
   // six quads of box() (quad.h:91-112) with one lambertian material -> one slab record
@@ -881,12 +883,14 @@ bool Compiler::flat_program(const std::vector<uint32_t>& lin, std::vector<FlatQu
       const int f = 2 * q.A + (q.plane == hi[q.A] ? 1 : 0);
       if (seen[f]++) return false;
       b.face[f] = q.e;
+      if (quads_[epay(q.e)].n[q.A] < 0) b.neg |= 1u << f;
     }
     for (int k = 0; k < 3; k++) {
       b.lo[k] = (float)(lo[k] + off[k]);
       b.hi[k] = (float)(hi[k] + off[k]);
     }
     b.inst = qs[0].inst;
+    b.mat = (uint32_t)mat;
     return true;
   };
   const double zero[3] = {0, 0, 0};
@@ -949,6 +953,7 @@ bool Compiler::flat_program(const std::vector<uint32_t>& lin, std::vector<FlatQu
   for (int a = 0; a < 3; a++) {
     if (grp[a].size() % 2) {  // pad to pairs: a NaN plane never hits
       FlatQuad pad{};
+      pad.nm = (uint32_t)a << 28;
       pad.plane = std::numeric_limits<float>::quiet_NaN();
       pad.e = kNoHit;
       pad.inst = -2;

@@ -103,7 +103,8 @@ _lib = None
 
 
 def lib_path():
-    return os.path.join(BUILD_DIR, "librt_hip.so")
+    # RT_HIP_LIB: a development build of the same library (scripts/build_variant.sh)
+    return os.environ.get("RT_HIP_LIB") or os.path.join(BUILD_DIR, "librt_hip.so")
 
 
 def load():
