@@ -77,7 +77,7 @@ def cpu_baseline(scene_name, width, aspect, spp, depth, seed, threads):
 
 
 def measured_traffic(workload):
-    """HBM bytes per k_step launch from the newest committed PMC summary of this exact workload
+    """HBM bytes per launch of the dominant kernel from the newest committed PMC summary of this exact workload
     (profiles/<round>_traffic.json, written by scripts/pmc_summary.py), or None."""
     found = None
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json"))):
@@ -100,10 +100,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
-    ap.add_argument("--pool", type=int, default=0, help="wavefront slots (0 = library default)")
+    ap.add_argument("--pool", type=int, default=0, help="path slots / persistent lanes (0 = library default)")
     ap.add_argument("--chunk", type=int, default=0, help="samples per work item (0 = library default)")
     ap.add_argument("--segments-per-launch", type=int, default=0,
-                    help="segments each path slot advances per k_step launch (0 = library default)")
+                    help="0: persistent schedule (one k_persist launch per frame); K > 0: "
+                         "wavefront k_step launches of K segments per path slot")
     ap.add_argument("--traversal", default="auto", choices=["auto", "ordered"],
                     help="ordered: the reference-ordered linear program / BVH also in fp32 (no flat program)")
     ap.add_argument("--seed", type=int, default=1)
@@ -194,7 +195,8 @@ def main():
     if rank == 0:
         my_samples = counts[0] * spp * args.steps
         seg_per_sample = segs / max(1, my_samples)
-        # dominant kernel of rank 0 (k_step: the fused extend+shade wavefront step): algorithmic bytes of
+        # dominant kernel of rank 0 (k_persist: the persistent extend+shade loop, one launch per frame;
+        # k_step with --segments-per-launch K: the fused wavefront step): algorithmic bytes of
         # SURVEY.md §8(d) per launch / average launch duration from HIP events on the render stream
         roof = None
         if args.kernel_timing == "on" and iters > 0:
@@ -202,7 +204,8 @@ def main():
             avg_s = step_ms / 1e3 / iters
             achieved = alg_bytes / (step_ms / 1e3) / 1e9
             mt = measured_traffic(workload_key(scene_name, W, H, spp, depth, args))
-            roof = {"bound": "hbm", "kernel": "k_step", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            kern = "k_step" if args.segments_per_launch > 0 else "k_persist"
+            roof = {"bound": "hbm", "kernel": kern, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": int(mt[1]) if mt else None,
                     "avg_launch_us": round(avg_s * 1e6, 2), "launches": iters,

@@ -1,8 +1,11 @@
 // rt_kernels.hip -- wavefront path tracer for MI355X (gfx950) + the C ABI of include/rt_hip.h.
 //
 // The reference's per-pixel/per-sample loop (camera.h:154-172) and recursive
-// ray_color (camera.h:193-241) become a pool of P path slots held in HBM as
-// structure-of-arrays (16-byte records per slot, coalesced dwordx4 access):
+// ray_color (camera.h:193-241) become P path slots. Default schedule (k_persist):
+// one launch of P lanes, each keeping its path in registers and walking items
+// lane, lane + P, ... Wavefront schedule (segments_per_launch = K > 0): the slots'
+// state lives in HBM as structure-of-arrays (16-byte records per slot, coalesced
+// dwordx4 access) between launches:
 //
 //   k_init    first camera ray of every slot            (camera.h:244-251)
 //   repeat:
@@ -52,6 +55,9 @@ constexpr uint32_t kAutoPool32 = 1u << 21;
 constexpr uint32_t kAutoPool64 = 1u << 19;
 constexpr uint32_t kAutoChunk = 16;
 constexpr int kAutoSegments = 16;  // segments each slot advances per k_step launch
+// persistent schedule: lanes in the grid (4 Mi, ~10x what the chip holds resident: blocks that
+// start late balance the uneven per-lane work; C2 1 Mi 20.2, 2 Mi 21.1, 4 Mi 21.4, 8 Mi 20.8 G/s)
+constexpr uint32_t kAutoPersistLanes = 1u << 22;
 
 template <class R>
 struct alignas(4 * sizeof(R)) R4 {
@@ -109,6 +115,10 @@ struct Params {
   const CamDev* camx;
   unsigned long long* seg_shards;
   int32_t K;  // segments per launch
+  // persistent mode (k_persist): one launch, lanes stride over the items by P
+  int32_t persist;
+  uint64_t seg_cap;  // a lane never needs more segments than this (its items * chunk * max_depth)
+  uint32_t* fault;   // set when a lane hits seg_cap (internal error, reported by the host)
   Light<R> light;  // copy of the scene's light: kernel arguments are read with scalar loads
 };
 
@@ -619,6 +629,60 @@ __device__ __forceinline__ void step_body(const Params<R>& p) {
   }
 }
 
+// Persistent form of the same loop (the default schedule): the grid is what the chip holds
+// resident, every lane keeps its path state in registers for the whole render and walks the
+// items lane, lane + P, lane + 2P, ... (P = grid lanes; shade's path regeneration does the
+// striding, as for a k_step slot). No state goes through HBM between segments, there is no
+// launch per K segments, no live-slot compaction and no shared work counter (one counter for
+// the whole chip serialises across the 8 XCDs' L2s: measured 6x slower on C2).
+template <class R, class Trav, bool CAMX>
+__device__ __forceinline__ void persist_body(const Params<R>& p) {
+  __shared__ Lds<Trav::kStack * kBlock> stk;
+  __shared__ uint32_t wave_cnt[kBlock / 64];
+  __shared__ Node<R> lds_nodes[Trav::kLdsNodes > 0 ? Trav::kLdsNodes : 1];
+  if constexpr (Trav::kLdsNodes > 0) {
+    for (uint32_t j = threadIdx.x; j < p.sc.n_nodes; j += kBlock) lds_nodes[j] = p.sc.nodes[j];
+    __syncthreads();
+  }
+  const uint32_t item0 = blockIdx.x * kBlock + threadIdx.x;
+  uint64_t segs = 0;
+  if (item0 < p.n_items) {
+    Path<R> s;
+    s.acc = mkv(R(0), R(0), R(0));
+    begin_item(p, s, item0);
+    begin_sample<R, CAMX>(p, s);
+#pragma unroll 1
+    for (;;) {
+      R t;
+      uint32_t e, nm = 0;
+      int32_t inst;
+      Trav::run(p.sc, lds_nodes, s, Keys{s.ks}, stk.v + threadIdx.x, t, e, inst, nm);
+      if (++segs > p.seg_cap) {  // cannot happen: every segment advances a bounce-capped path
+        atomicOr(p.fault, 1u);
+        break;
+      }
+      if (!shade<R, CAMX, Trav::kFlat>(p, s, t, e, inst, nm)) break;
+    }
+  }
+  uint32_t sg = (uint32_t)segs;
+  for (int off = 32; off > 0; off >>= 1) sg += __shfl_xor(sg, off);
+  if ((threadIdx.x & 63) == 0) wave_cnt[threadIdx.x >> 6] = sg;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t c = (uint64_t)wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3];
+    if (c) atomicAdd(&p.seg_shards[blockIdx.x % kSegShards], (unsigned long long)c);
+  }
+}
+template <class R, class Trav, bool CAMX>
+__global__ __launch_bounds__(kBlock) void k_persist(Params<R> p) {
+  persist_body<R, Trav, CAMX>(p);
+}
+template <class R, class Trav, bool CAMX>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Trav::kWaves))) void k_persist_occ(
+    Params<R> p) {
+  persist_body<R, Trav, CAMX>(p);
+}
+
 // The kernel; k_step_occ is the same body with the register budget cut for Trav::kWaves
 // waves per SIMD (only where that does not spill much, see LinearTrav::kWaves).
 // CAMX ("extended"): a non-perspective camera (camera_ray) or procedural textures (noise.h); the
@@ -873,16 +937,33 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
   return s;
 }
 
+template <class KernelT, class R>
+void launch_one(KernelT kern, Params<R> p, uint32_t grid, hipStream_t st) {
+  if (p.persist) {  // the lanes stride over the items by the grid's lane count
+    p.P = grid * kBlock;
+    p.seg_cap = ((uint64_t)p.n_items + p.P - 1) / p.P * p.chunk * (uint64_t)p.max_depth + 1;
+  }
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, st, p);
+}
 template <class R, class Trav>
 void launch_k(const Params<R>& p, uint32_t grid, hipStream_t st) {
   const bool camx = p.cam_mode != RT_CAM_PERSPECTIVE || p.sc.has_procedural;
   // the extended kernels run without the occupancy budget (their noise / camera code would spill)
-  if (camx)
-    hipLaunchKernelGGL((k_step<R, Trav, true>), dim3(grid), dim3(kBlock), 0, st, p);
-  else if constexpr (Trav::kWaves > 1)
-    hipLaunchKernelGGL((k_step_occ<R, Trav, false>), dim3(grid), dim3(kBlock), 0, st, p);
-  else
-    hipLaunchKernelGGL((k_step<R, Trav, false>), dim3(grid), dim3(kBlock), 0, st, p);
+  if (p.persist) {
+    if (camx)
+      launch_one(k_persist<R, Trav, true>, p, grid, st);
+    else if constexpr (Trav::kWaves > 1)
+      launch_one(k_persist_occ<R, Trav, false>, p, grid, st);
+    else
+      launch_one(k_persist<R, Trav, false>, p, grid, st);
+  } else {
+    if (camx)
+      launch_one(k_step<R, Trav, true>, p, grid, st);
+    else if constexpr (Trav::kWaves > 1)
+      launch_one(k_step_occ<R, Trav, false>, p, grid, st);
+    else
+      launch_one(k_step<R, Trav, false>, p, grid, st);
+  }
 }
 
 template <class R>
@@ -891,7 +972,7 @@ void launch_step(const Params<R>& p, int stack, bool sph, bool tri, uint32_t gri
   if constexpr (sizeof(R) == 4) {
     // the flat program (world-space quads and boxes); the extended kernels keep the linear one
     if (p.sc.has_flat && p.cam_mode == RT_CAM_PERSPECTIVE && !p.sc.has_procedural) {
-      hipLaunchKernelGGL((k_step_occ<float, FlatTrav, false>), dim3(grid), dim3(kBlock), 0, st, p);
+      launch_k<float, FlatTrav>(p, grid, st);
       return;
     }
   }
@@ -952,18 +1033,25 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     const uint64_t n_items64 = (uint64_t)npix * nchunks;
     if (n_items64 >= (1ull << 31)) return set_err(c, RT_ERR_INVALID_ARGUMENT, "too many work items in one call");
     const uint32_t n_items = (uint32_t)n_items64;
-    uint32_t P = prm->pool_slots > 0 ? (uint32_t)prm->pool_slots : (f64 ? kAutoPool64 : kAutoPool32);
+    // the default schedule is persistent (k_persist); an explicit segments_per_launch selects the
+    // launch-per-K-segments wavefront with HBM path state and live-slot compaction
+    const bool persist = prm->segments_per_launch <= 0;
+    uint32_t P = prm->pool_slots > 0 ? (uint32_t)prm->pool_slots
+                 : persist       ? kAutoPersistLanes
+                                 : (f64 ? kAutoPool64 : kAutoPool32);
     P = std::max<uint32_t>(1, std::min(P, n_items));
     const uint32_t nblk_max = (P + kBlock - 1) / kBlock;
 
     // path state: 5 R4 arrays (O, D, T, L, A) + uint4 keys (S) + uint4 exclusion/pixel (X), each P long
     auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
     const size_t r4 = al(sizeof(R4<R>) * (size_t)P), sb = al(16 * (size_t)P), xb = al(16 * (size_t)P);
-    if ((s = ensure(c, c->state, 5 * r4 + sb + xb)) != RT_OK) return s;
+    if (!persist) {
+      if ((s = ensure(c, c->state, 5 * r4 + sb + xb)) != RT_OK) return s;
+      if ((s = ensure(c, c->queue0, 4ull * P)) != RT_OK) return s;
+      if ((s = ensure(c, c->queue1, 4ull * P)) != RT_OK) return s;
+    }
     if ((s = ensure(c, c->partial, 3ull * n_items * sizeof(R))) != RT_OK) return s;
     if ((s = ensure(c, c->pixmap, 4ull * npix)) != RT_OK) return s;
-    if ((s = ensure(c, c->queue0, 4ull * P)) != RT_OK) return s;
-    if ((s = ensure(c, c->queue1, 4ull * P)) != RT_OK) return s;
     if ((s = ensure(c, c->blk, 4ull * (nblk_max + 2))) != RT_OK) return s;
     RT_HIP(c, hipMemcpyAsync(c->pixmap.ptr, pix.data(), 4ull * npix, hipMemcpyHostToDevice, st));
     RT_HIP(c, hipMemsetAsync(c->counters.ptr, 0, sizeof(unsigned long long) * kSegShards, st));
@@ -995,28 +1083,53 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     p.max_depth = prm->max_depth;
     p.seed = prm->seed;
     c->cam_host = make_view(cam);
-    if ((s = ensure(c, c->camx, sizeof(CamDev))) != RT_OK) return s;
-    RT_HIP(c, hipMemcpyAsync(c->camx.ptr, &c->cam_host, sizeof(CamDev), hipMemcpyHostToDevice, st));
     p.cpos = c->cam_host.pos;
     p.cdu = c->cam_host.du;
     p.cdv = c->cam_host.dv;
     p.cdir00 = c->cam_host.dir00;
+    if ((s = ensure(c, c->camx, sizeof(CamDev))) != RT_OK) return s;
+    RT_HIP(c, hipMemcpyAsync(c->camx.ptr, &c->cam_host, sizeof(CamDev), hipMemcpyHostToDevice, st));
     p.cam_mode = c->cam_host.mode;
     p.camx = (const CamDev*)c->camx.ptr;
     p.seg_shards = (unsigned long long*)c->counters.ptr;
     const int K = prm->segments_per_launch > 0 ? std::min(prm->segments_per_launch, 64) : kAutoSegments;
     p.K = K;
-
+    uint64_t launches = 0, iters = 0;
+    size_t ev = 0;
+    if (persist) {
+      // one launch of P lanes (pool_slots, or kAutoPersistLanes)
+      uint32_t* ctr = (uint32_t*)c->blk.ptr;
+      RT_HIP(c, hipMemsetAsync(ctr, 0, 8, st));
+      p.persist = 1;
+      p.fault = ctr + 1;
+      const uint32_t grid = nblk_max;
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      if (c->timing) {
+        e0 = take_event(c, 0);
+        e1 = take_event(c, 1);
+        if (!e0 || !e1) return set_err(c, RT_ERR_HIP, "hipEventCreate failed");
+        RT_HIP(c, hipEventRecord(e0, st));
+      }
+      launch_step<R>(p, cs.stack_need, hdr.n_spheres > 0, hdr.n_tris > 0, grid, st);
+      RT_HIP(c, hipGetLastError());
+      if (c->timing) {
+        RT_HIP(c, hipEventRecord(e1, st));
+        ev = 2;
+      }
+      launches = iters = 1;
+      RT_HIP(c, hipMemcpyAsync(c->total_host, ctr + 1, 4, hipMemcpyDeviceToHost, st));
+      RT_HIP(c, hipStreamSynchronize(st));
+      if (*c->total_host) return set_err(c, RT_ERR_HIP, "a path did not finish (internal error)");
+    } else {
     if (p.cam_mode != RT_CAM_PERSPECTIVE || p.sc.has_procedural)
       hipLaunchKernelGGL((k_init<R, true>), dim3(nblk_max), dim3(kBlock), 0, st, p);
     else
       hipLaunchKernelGGL((k_init<R, false>), dim3(nblk_max), dim3(kBlock), 0, st, p);
-    uint64_t launches = 1, iters = 0;
+    launches = 1;
     uint32_t* qbuf[2] = {(uint32_t*)c->queue0.ptr, (uint32_t*)c->queue1.ptr};
     int qsel = 0;
     uint32_t* blk = (uint32_t*)c->blk.ptr;
     uint32_t* d_total = blk + nblk_max + 1;
-    size_t ev = 0;
     // every slot finishes within (items per slot) * chunk * max_depth segments; anything longer is a bug
     const uint64_t iter_cap =
         (((uint64_t)(n_items + P - 1) / P) * chunk * (uint64_t)prm->max_depth + K - 1) / K + 4 * kBatch;
@@ -1056,6 +1169,7 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
         p.n = alive;
       }
     }
+    }  // !persist
     hipLaunchKernelGGL(k_resolve<R>, dim3((npix + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
                        (const R*)c->partial.ptr, npix, nchunks, spp, (R*)dout);
     launches++;

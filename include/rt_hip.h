@@ -179,9 +179,12 @@ typedef struct rt_render_params {
   int32_t first_sample;     /* render samples [first_sample, first_sample + spp) of each pixel */
   int32_t samples_per_item; /* samples one work item accumulates (0 = auto: min(spp, 16)). The per-pixel sum
                                is grouped by item, so this changes the image only by rounding. */
-  int32_t pool_slots;       /* wavefront pool size (0 = auto). Does not change the image. */
-  int32_t segments_per_launch; /* segments each path slot advances per kernel launch (0 = auto).
-                                  Does not change the image. */
+  int32_t pool_slots;       /* path slots: lanes of the persistent kernel, or the wavefront pool
+                               (0 = auto). Does not change the image. */
+  int32_t segments_per_launch; /* 0 = the persistent schedule (one launch, path state in registers);
+                                  K > 0 = the wavefront schedule: each path slot advances up to K
+                                  segments per launch, state in HBM between launches, live-slot
+                                  compaction. Does not change the image. */
   int32_t traversal;        /* rt_traversal: 0 = auto. RT_TRAV_ORDERED keeps the reference-ordered
                                linear program / BVH in fp32 too (the fp32 flat program of quad/box
                                scenes differs from it only in exact-t ties and rounding). */

@@ -6,12 +6,12 @@
 Writes
   profiles/<tag>_kernel_stats.csv   the --kernel-trace --stats summary (copied as rocprofv3 wrote it)
   profiles/<tag>_pmc_summary.csv    per kernel and counter: dispatches, mean and total over the run
-  profiles/<tag>_traffic.json       HBM bytes per k_step launch, read by bench.py for roofline.traffic
+  profiles/<tag>_traffic.json       HBM bytes per launch of the dominant kernel, read by bench.py for roofline.traffic
 
 HBM bytes follow MI355X_MICROARCH.md (HBM [CDNA4]): FETCH_SIZE and WRITE_SIZE are in KiB,
 and on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced read, so
 bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024. FETCH_SIZE and WRITE_SIZE come from
-separate passes (they do not fit one pass), averaged over the same k_step launches.
+separate passes (they do not fit one pass), averaged over the same launches.
 """
 import csv
 import glob
@@ -51,15 +51,16 @@ def main():
         w = csv.writer(fh)
         w.writerow(["kernel", "counter", "dispatches", "mean", "total"])
         w.writerows(rows)
-    # the dominant kernel: all k_step instantiations of the run
+    # the dominant kernel: all k_persist (default schedule) or k_step instantiations of the run
+    fam = "k_persist" if any(k.startswith("k_persist") for k in acc) else "k_step"
     fetch, write = [], []
     for k, counters in acc.items():
-        if k.startswith("k_step"):
+        if k.startswith(fam):
             fetch += counters.get("FETCH_SIZE", [])
             write += counters.get("WRITE_SIZE", [])
     if fetch and write:
         f_mean, w_mean = sum(fetch) / len(fetch), sum(write) / len(write)
-        traffic = {"kernel": "k_step", "workload": workload, "launches_fetch_pass": len(fetch),
+        traffic = {"kernel": fam, "workload": workload, "launches_fetch_pass": len(fetch),
                    "launches_write_pass": len(write), "fetch_size_kib_mean": f_mean, "write_size_kib_mean": w_mean,
                    "bytes_per_launch": (2.0 * f_mean + w_mean) * 1024.0,
                    "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (KiB; gfx950 FETCH_SIZE counts half, "

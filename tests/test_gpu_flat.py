@@ -107,5 +107,6 @@ def test_flat_program_invariant_to_schedule(ctx):
     desc, cam, _, _ = scenes.cornell_box(width=70)
     ctx.upload(desc)
     base = ctx.render(cam, 12, 6, seed=3, precision=F32)
-    for kw in [dict(pool_slots=1000, segments_per_launch=1), dict(pool_slots=1 << 16, segments_per_launch=64)]:
+    for kw in [dict(pool_slots=1000, segments_per_launch=1), dict(pool_slots=1 << 16, segments_per_launch=64),
+               dict(pool_slots=333)]:
         assert np.array_equal(ctx.render(cam, 12, 6, seed=3, precision=F32, **kw), base), kw

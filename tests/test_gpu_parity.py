@@ -107,9 +107,9 @@ def test_image_invariant_to_schedule_and_tiling(ctx, precision):
     desc, cam, _, _ = scenes.cornell_box_with_volume(width=70)
     ctx.upload(desc)
     base = ctx.render(cam, 12, 6, seed=3, precision=precision)
-    # pool size and segments per launch change only the schedule: bit-identical
+    # the schedule (persistent lanes, or wavefront pool size and segments per launch): bit-identical
     for kw in [dict(pool_slots=1000, segments_per_launch=1), dict(pool_slots=777, segments_per_launch=3),
-               dict(pool_slots=1 << 16, segments_per_launch=64)]:
+               dict(pool_slots=1 << 16, segments_per_launch=64), dict(pool_slots=777), dict(pool_slots=64)]:
         assert np.array_equal(ctx.render(cam, 12, 6, seed=3, precision=precision, **kw), base), kw
     # the item size regroups each pixel's sum: equal up to rounding
     for chunk in (1, 5):
