@@ -168,8 +168,10 @@ __host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   x ^= x >> 16;
   x *= 0x21f0aaadu;
   x ^= x >> 15;
+#ifndef RT_EXP_CHEAPMIX  // timing experiment only (wrong images)
   x *= 0xd35a2d97u;
   x ^= x >> 15;
+#endif
   return x;
 }
 __host__ __device__ __forceinline__ uint32_t key_pixel(uint64_t seed, uint32_t pixel) {
@@ -405,6 +407,20 @@ __device__ __forceinline__ T ld_uniform(const T* p, uint32_t i) {
   return ((const __attribute__((address_space(4))) T*)p)[i];
 #else
   return p[i];  // host pass of a device function: never executed
+#endif
+}
+// ld_uniform at the point of use: the index is an opaque zero, so the scalar load cannot be
+// hoisted out of the path loop. Loop-invariant uniforms (the light, the camera) hoisted to the
+// kernel entry outlive the SGPR budget and are spilled into VGPR lanes, and every use then costs
+// a v_readlane (a VALU issue slot); a scalar reload from the constant cache costs none.
+template <class T>
+__device__ __forceinline__ T ld_here(const T* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t z;
+  asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+  return ((const __attribute__((address_space(4))) T*)p)[z];
+#else
+  return *p;
 #endif
 }
 
@@ -1044,45 +1060,67 @@ __device__ __forceinline__ V<R> cosine_dir(R r1, R r2) {
 // light at t = 1 by construction, and fp32 uses that instead of re-testing: a point sampled on
 // the light's edge (u1 or u2 ~ 0) can round to just outside it, giving pdf 0 for a direction
 // the light itself produced (and 0/0 = NaN when the material pdf is 0 too).
+// The light is read where it is used, field group by field group (ld_here), so no light data
+// stays live across the path loop (it would be spilled to VGPR lanes).
 template <class R>
-__device__ __forceinline__ R light_pdf(const Light<R>& L, V<R> o, V<R> dir, bool sampled = false) {
-  if (L.kind == L_QUAD) {
+struct R4s {
+  R v[4];
+};
+template <class R>
+struct LightUV {  // Light::u, pad1, v, pad2
+  R u[3], pad1, v[3], pad2;
+};
+template <class R>
+struct LightAF {  // Light::af
+  R f[8];
+};
+template <class R>
+__device__ __forceinline__ R light_pdf(const Light<R>* Lp, V<R> o, V<R> dir, bool sampled = false) {
+  const int32_t kind = ld_here(&Lp->kind);
+  if (kind == L_QUAD) {
     R t;
     bool hit;
+    const int32_t aligned = ld_here(&Lp->aligned);
     if (sizeof(R) == 4 && sampled) {
       t = R(1);
       hit = true;
-    } else if (sizeof(R) == 4 && L.aligned) {  // uniform branch: the light is a kernel argument
+    } else if (sizeof(R) == 4 && aligned) {  // uniform branch
+      const LightAF<R> af = ld_here(reinterpret_cast<const LightAF<R>*>(Lp->af));
       const V<R> inv = rcp3(dir);
-      switch (L.aligned) {
-        case 1: hit = aquad_t<2, 0, 1>(L.af, o, dir, inv, R(0.001), Num<R>::inf(), t); break;
-        case 2: hit = aquad_t<1, 0, 2>(L.af, o, dir, inv, R(0.001), Num<R>::inf(), t); break;
-        case 3: hit = aquad_t<2, 1, 0>(L.af, o, dir, inv, R(0.001), Num<R>::inf(), t); break;
-        case 4: hit = aquad_t<0, 1, 2>(L.af, o, dir, inv, R(0.001), Num<R>::inf(), t); break;
-        case 5: hit = aquad_t<1, 2, 0>(L.af, o, dir, inv, R(0.001), Num<R>::inf(), t); break;
-        default: hit = aquad_t<0, 2, 1>(L.af, o, dir, inv, R(0.001), Num<R>::inf(), t); break;
+      switch (aligned) {
+        case 1: hit = aquad_t<2, 0, 1>(af.f, o, dir, inv, R(0.001), Num<R>::inf(), t); break;
+        case 2: hit = aquad_t<1, 0, 2>(af.f, o, dir, inv, R(0.001), Num<R>::inf(), t); break;
+        case 3: hit = aquad_t<2, 1, 0>(af.f, o, dir, inv, R(0.001), Num<R>::inf(), t); break;
+        case 4: hit = aquad_t<0, 1, 2>(af.f, o, dir, inv, R(0.001), Num<R>::inf(), t); break;
+        case 5: hit = aquad_t<1, 2, 0>(af.f, o, dir, inv, R(0.001), Num<R>::inf(), t); break;
+        default: hit = aquad_t<0, 2, 1>(af.f, o, dir, inv, R(0.001), Num<R>::inf(), t); break;
       }
     } else {
-      hit = quad_t(L.quad, o, dir, R(0.001), Num<R>::inf(), t);
+      hit = quad_t(ld_here(&Lp->quad), o, dir, R(0.001), Num<R>::inf(), t);
     }
     if (!hit) return R(0);
+    const Quad<R> q = ld_here(&Lp->quad);
     R dist2 = t * t * dot(dir, dir);
-    R cosine = fabs(dot(unit(dir), ld3(L.quad.n)));
-    return fdiv(dist2, cosine * L.quad.area);
+    R cosine = fabs(dot(unit(dir), ld3(q.n)));
+    return fdiv(dist2, cosine * q.area);
   }
-  if (L.kind == L_SPHERE) {
-    V<R> f = o - ld3(L.center);
-    return fdiv(L.radius * L.radius * Num<R>::pi(), dot(f, f));
+  if (kind == L_SPHERE) {
+    const R4s<R> c = ld_here(reinterpret_cast<const R4s<R>*>(Lp->center));  // center[3], radius
+    V<R> f = o - mkv(c.v[0], c.v[1], c.v[2]);
+    return fdiv(c.v[3] * c.v[3] * Num<R>::pi(), dot(f, f));
   }
   return R(0);
 }
 template <class R>
-__device__ __forceinline__ V<R> light_random(const Light<R>& L, V<R> o, R u1, R u2) {
-  if (L.kind == L_QUAD) {
-    V<R> p = (ld3(L.quad.q) + u1 * ld3(L.u)) + u2 * ld3(L.v);
+__device__ __forceinline__ V<R> light_random(const Light<R>* Lp, V<R> o, R u1, R u2) {
+  const int32_t kind = ld_here(&Lp->kind);
+  if (kind == L_QUAD) {
+    const Quad<R> q = ld_here(&Lp->quad);
+    const LightUV<R> uv = ld_here(reinterpret_cast<const LightUV<R>*>(Lp->u));
+    V<R> p = (ld3(q.q) + u1 * ld3(uv.u)) + u2 * ld3(uv.v);
     return p - o;
   }
-  if (L.kind == L_SPHERE) return on_sphere(u1, u2) * L.radius;
+  if (kind == L_SPHERE) return on_sphere(u1, u2) * ld_here(&Lp->radius);
   return mkv(R(1), R(0), R(0));
 }
 

@@ -43,6 +43,9 @@ using namespace rtd;
 namespace {
 
 constexpr int kBlock = 256;
+#ifndef RT_CAM_BASE
+#define RT_CAM_BASE 1
+#endif
 #ifndef RT_LINEAR_WAVES
 #define RT_LINEAR_WAVES 6
 #endif
@@ -108,9 +111,8 @@ struct Params {
   uint32_t npix_k;
   int32_t max_depth;
   uint64_t seed;
-  // camera rays are built in fp64 for both paths (fp32 rounds once): the perspective camera
-  // from kernel arguments; the other models read the rest of CamDev (device memory, scalar loads)
-  V<double> cpos, cdu, cdv, cdir00;
+  // camera rays are built in fp64 for both paths (fp32 rounds once), from CamDev in device
+  // memory (scalar loads at the point of use)
   int32_t cam_mode;
   const CamDev* camx;
   unsigned long long* seg_shards;
@@ -119,7 +121,6 @@ struct Params {
   int32_t persist;
   uint64_t seg_cap;  // a lane never needs more segments than this (its items * chunk * max_depth)
   uint32_t* fault;   // set when a lane hits seg_cap (internal error, reported by the host)
-  Light<R> light;  // copy of the scene's light: kernel arguments are read with scalar loads
 };
 
 template <class R>
@@ -131,7 +132,21 @@ struct Path {
   uint32_t xe;
   int32_t xi;
   uint32_t xy, send;
+#if RT_CAM_BASE
+  V<double> cb;  // (dir00 + x du) + y dv of the item's pixel (pixel_base)
+#endif
 };
+
+// The pixel's part of the perspective camera ray, (dir00 + x du) + y dv (camera.h:246-250): the
+// same for every sample of a work item, so it is computed once per item (and once per k_step
+// launch), not once per sample. Same operations in the same order: bit-identical.
+template <class R>
+__device__ __forceinline__ void pixel_base(const Params<R>& p, Path<R>& s) {
+#if RT_CAM_BASE
+  const double x = double(s.xy & 0xFFFFu), y = double(s.xy >> 16);
+  s.cb = (ld_here(&p.camx->dir00) + x * ld_here(&p.camx->du)) + y * ld_here(&p.camx->dv);
+#endif
+}
 
 template <class R>
 __device__ __forceinline__ void load_path(const Params<R>& p, uint32_t slot, R4<R> Dv, Path<R>& s) {
@@ -153,6 +168,7 @@ __device__ __forceinline__ void load_path(const Params<R>& p, uint32_t slot, R4<
   s.xi = (int32_t)X.y;
   s.xy = X.z;
   s.send = X.w;
+  pixel_base(p, s);
 }
 
 template <class R>
@@ -177,6 +193,7 @@ __device__ __forceinline__ void begin_item(const Params<R>& p, Path<R>& s, uint3
   s.send = min(s.sample + p.chunk, p.spp);
   s.xy = xy;
   s.ka = key_pixel(p.seed, (xy >> 16) * p.W + (xy & 0xFFFFu));
+  pixel_base(p, s);
 }
 
 // camera::generate_ray for the orthonormal, fisheye and lens models (camera.h:252-290), reading
@@ -232,10 +249,15 @@ __device__ __forceinline__ void begin_sample(const Params<R>& p, Path<R>& s) {
   // camera ray, which otherwise shows up as paths crossing a checker line or edge differently.
   const double ox = to_unit<double>(draw_u32(s.ks, 0)) - 0.5;  // sample_square (camera.h:293)
   const double oy = to_unit<double>(draw_u32(s.ks, 1)) - 0.5;
-  V<double> o = p.cpos, d;
+  V<double> o = ld_here(&p.camx->pos), d;
   double tm;
   if (!CAMX || p.cam_mode == RT_CAM_PERSPECTIVE) {  // camera.h:245-251
-    d = ((p.cdir00 + double(x) * p.cdu) + double(y) * p.cdv + ox * p.cdu) + oy * p.cdv;
+    const V<double> du = ld_here(&p.camx->du), dv = ld_here(&p.camx->dv);
+#if RT_CAM_BASE
+    d = (s.cb + ox * du) + oy * dv;
+#else
+    d = ((ld_here(&p.camx->dir00) + double(x) * du) + double(y) * dv + ox * du) + oy * dv;
+#endif
     tm = to_unit<double>(draw_u32(s.ks, 2));
   } else if constexpr (CAMX) {
     camera_ray(p.camx, s.ks, x, y, ox, oy, o, d, tm);
@@ -436,10 +458,10 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
         const R iso_pdf = R(1) / (R(4) * Num<R>::pi());
         Onb<R> b;
         if (!iso) b = make_onb(n);
-        const Light<R>& Lt = p.light;
+        const Light<R>* Lt = sc.light;  // read at the point of use (light_pdf, light_random)
         R pv;
         V<R> dir;
-        if (Lt.kind == L_NONE) {  // camera.h:217-226
+        if (ld_here(&Lt->kind) == L_NONE) {  // camera.h:217-226
           R u1 = U();
           R u2 = U();
           dir = iso ? unit(on_sphere(u1, u2)) : onb_transform(b, cosine_dir(u1, u2));
@@ -1060,7 +1082,6 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     Params<R> p{};
     p.sc = dev_scene<R>(hdr, sbase);
     if (prm->traversal == RT_TRAV_ORDERED) p.sc.has_flat = 0;
-    std::memcpy(&p.light, (f64 ? cs.blob64 : cs.blob32).data() + hdr.off_light, sizeof(Light<R>));
     p.O = (R4<R>*)sp;
     p.D = (R4<R>*)(sp + r4);
     p.T = (R4<R>*)(sp + 2 * r4);
@@ -1083,10 +1104,6 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     p.max_depth = prm->max_depth;
     p.seed = prm->seed;
     c->cam_host = make_view(cam);
-    p.cpos = c->cam_host.pos;
-    p.cdu = c->cam_host.du;
-    p.cdv = c->cam_host.dv;
-    p.cdir00 = c->cam_host.dir00;
     if ((s = ensure(c, c->camx, sizeof(CamDev))) != RT_OK) return s;
     RT_HIP(c, hipMemcpyAsync(c->camx.ptr, &c->cam_host, sizeof(CamDev), hipMemcpyHostToDevice, st));
     p.cam_mode = c->cam_host.mode;
