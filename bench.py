@@ -3,7 +3,7 @@
 
 Workload (BASELINE.json configs[1]): the reference's Cornell Box
 (main.cc:198-225) at 800x800, 1024 spp, max depth 50, light importance sampling on.
-One step = one full frame. The framebuffer is cut into 64x64 tiles dealt
+One step = one full frame. The framebuffer is cut into 32x32 tiles dealt
 round-robin to the ranks; each rank renders its tiles on its GPU and rank 0
 gathers them (RCCL, torch.distributed "nccl") into the full linear framebuffer.
 
@@ -76,14 +76,15 @@ def cpu_baseline(scene_name, width, aspect, spp, depth, seed, threads):
                       f"{cam.image_width} px x {spp} spp, depth {depth}: {n / 1e6:.1f} Msamples in {dt:.1f} s"}
 
 
-def measured_traffic(workload):
-    """HBM bytes per launch of the dominant kernel from the newest committed PMC summary of this exact workload
-    (profiles/<round>_traffic.json, written by scripts/pmc_summary.py), or None."""
+def measured_traffic(workload, kernel):
+    """HBM bytes per launch of the dominant kernel from the committed PMC summary of this exact workload and
+    kernel family (profiles/<tag>_traffic.json, written by scripts/pmc_summary.py; the last in name order
+    wins), or None."""
     found = None
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json"))):
         with open(f) as fh:
             d = json.load(fh)
-        if d.get("workload") == workload:
+        if d.get("workload") == workload and d.get("kernel") == kernel:
             found = (os.path.basename(f), d["bytes_per_launch"])
     return found
 
@@ -203,8 +204,8 @@ def main():
             alg_bytes = (B_GEN + B_ACC) * my_samples + (B_EXT + B_SHADE) * segs
             avg_s = step_ms / 1e3 / iters
             achieved = alg_bytes / (step_ms / 1e3) / 1e9
-            mt = measured_traffic(workload_key(scene_name, W, H, spp, depth, args))
             kern = "k_step" if args.segments_per_launch > 0 else "k_persist"
+            mt = measured_traffic(workload_key(scene_name, W, H, spp, depth, args), kern)
             roof = {"bound": "hbm", "kernel": kern, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": int(mt[1]) if mt else None,
@@ -226,7 +227,7 @@ def main():
             "data": asset or "synthetic (the reference's scene, procedurally built; no assets)",
             "config": {"workload": f"{scene_name} {W}x{H} {spp}spp depth {depth}, light sampling on",
                        "key": workload_key(scene_name, W, H, spp, depth, args),
-                       "image": [W, H], "spp": spp, "max_depth": depth, "tiles": "64x64 round-robin over ranks",
+                       "image": [W, H], "spp": spp, "max_depth": depth, "tiles": "32x32 round-robin over ranks",
                        "parallelism": f"tiles{world}", "segments_per_sample": round(seg_per_sample, 4),
                        "segments_total": segs_total / args.steps, "kernel_timing": args.kernel_timing,
                        "rounds_per_frame": iters // max(1, args.steps)},

@@ -2,8 +2,8 @@
 //
 // The reference's per-pixel/per-sample loop (camera.h:154-172) and recursive
 // ray_color (camera.h:193-241) become P path slots. Default schedule (k_persist):
-// one launch of P lanes, each keeping its path in registers and walking items
-// lane, lane + P, ... Wavefront schedule (segments_per_launch = K > 0): the slots'
+// one launch of as many lanes as the chip holds resident, each keeping its path in
+// registers and pulling work items from per-XCD dequeue heads. Wavefront schedule (segments_per_launch = K > 0): the slots'
 // state lives in HBM as structure-of-arrays (16-byte records per slot, coalesced
 // dwordx4 access) between launches:
 //
@@ -17,7 +17,7 @@
 //     (wave __ballot + block prefix sums) once half the pool has drained
 //   k_resolve  per-pixel mean over the chunks, in chunk order (camera.h:169-170)
 //
-// Work item = (pixel, chunk of C consecutive samples); slot s owns items
+// Work item = (pixel, chunk of C consecutive samples); a wavefront slot s owns items
 // s, s + P, s + 2P, ... Each sample's random numbers are keyed by
 // (seed, global pixel, sample) so the image is bit-identical for any pool size,
 // tiling or GPU count.
@@ -49,6 +49,9 @@ constexpr int kBlock = 256;
 #ifndef RT_LINEAR_WAVES
 #define RT_LINEAR_WAVES 6
 #endif
+#ifndef RT_PERSIST_MODE  // 2: dynamic (per-XCD heads), 1: static striding (development A/B)
+#define RT_PERSIST_MODE 2
+#endif
 #ifndef RT_STACK_WAVES
 #define RT_STACK_WAVES 3
 #endif
@@ -58,9 +61,19 @@ constexpr uint32_t kAutoPool32 = 1u << 21;
 constexpr uint32_t kAutoPool64 = 1u << 19;
 constexpr uint32_t kAutoChunk = 16;
 constexpr int kAutoSegments = 16;  // segments each slot advances per k_step launch
-// persistent schedule: lanes in the grid (4 Mi, ~10x what the chip holds resident: blocks that
-// start late balance the uneven per-lane work; C2 1 Mi 20.2, 2 Mi 21.1, 4 Mi 21.4, 8 Mi 20.8 G/s)
+// persistent schedule: upper bound of the grid's lanes. The dynamic schedule (persist 2) cuts the
+// grid to what the chip holds resident; the static one (persist 1) launches them all (~10x the
+// resident lanes: blocks that start late balance the uneven per-lane work)
 constexpr uint32_t kAutoPersistLanes = 1u << 22;
+
+// dynamic persistent schedule (persist 2): items are handed out in batches of kQBatch; batch j of
+// head h is batch number j * kHeads + h of the item space, so the heads interleave over the whole
+// frame and a head that runs dry steals from the others. Against static striding (persist 1) the
+// tail shrinks to one item: C2 28.6 -> 26.5 ms on one GPU, 4.07 -> 3.70 ms for one rank of eight.
+constexpr uint32_t kHeads = 8;
+constexpr uint32_t kHeadStride = 64;  // 256 B apart: one L2 line per head
+constexpr uint32_t kQBatch = 64;
+constexpr uint32_t kNoItem = 0xFFFFFFFFu;
 
 template <class R>
 struct alignas(4 * sizeof(R)) R4 {
@@ -117,8 +130,10 @@ struct Params {
   const CamDev* camx;
   unsigned long long* seg_shards;
   int32_t K;  // segments per launch
-  // persistent mode (k_persist): one launch, lanes stride over the items by P
+  // persistent mode (k_persist): one launch. 1: lanes stride over the items by P; 2 (default):
+  // the grid is what the chip holds resident and lanes pull items from the per-XCD heads
   int32_t persist;
+  uint32_t* heads;  // kHeads dequeue counters, kHeadStride words apart (persist 2)
   uint64_t seg_cap;  // a lane never needs more segments than this (its items * chunk * max_depth)
   uint32_t* fault;   // set when a lane hits seg_cap (internal error, reported by the host)
 };
@@ -181,6 +196,65 @@ __device__ __forceinline__ void store_path(const Params<R>& p, uint32_t slot, co
   p.A[slot] = {s.acc.x, s.acc.y, s.acc.z, R(0)};
   p.S[slot] = make_uint4(s.ka, s.ks, s.item, s.sample);
   p.X[slot] = make_uint4(s.xe, (uint32_t)s.xi, s.xy, s.send);
+}
+
+// The wave's local queue [next, end) of the dynamic schedule, in LDS (two words per wave).
+__device__ __forceinline__ uint32_t* wave_queue() {
+  __shared__ uint32_t wq[2 * (kBlock / 64)];
+  return wq + 2 * (threadIdx.x >> 6);
+}
+
+// A batch of kQBatch items for the calling lane's wave: the block's own head first (blocks b and
+// b + 8 share an XCD, so a head's counter stays in one XCD's traffic), then the others. Returns the
+// first item, or kNoItem once every head has run past the item space.
+__device__ __forceinline__ uint32_t grab_batch(uint32_t* heads, uint32_t n_items) {
+  const uint32_t g = blockIdx.x & (kHeads - 1);
+  for (uint32_t t = 0; t < kHeads; t++) {
+    const uint32_t h = (g + t) & (kHeads - 1);
+    const uint32_t j = atomicAdd(heads + h * kHeadStride, 1u);
+    const uint64_t first = ((uint64_t)j * kHeads + h) * kQBatch;
+    if (first < n_items) return (uint32_t)first;
+  }
+  return kNoItem;
+}
+
+// The next item of each calling lane (the lanes of the wave that finished an item in this
+// call, in divergent code): consecutive items from the wave's queue, refilled one batch at a
+// time by the lowest calling lane. Every value below is identical in the calling lanes.
+// kNoItem: the frame is exhausted and the lane retires (queue state [kNoItem, kNoItem)).
+template <class R>
+__device__ __forceinline__ uint32_t next_item_dyn(const Params<R>& p) {
+  uint32_t* wq = wave_queue();
+  const uint64_t need = __ballot(1);
+  const uint32_t lane = __lane_id();
+  const uint32_t k = (uint32_t)__popcll(need);
+  const uint32_t r = (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
+  const uint32_t leader = (uint32_t)__ffsll((unsigned long long)need) - 1;
+  uint32_t qn = __hip_atomic_load(wq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+  uint32_t qe = __hip_atomic_load(wq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+  uint32_t item = kNoItem, off = 0;
+  for (;;) {
+    const uint32_t rem = qe - qn;
+    if (r >= off && r - off < rem) item = qn + (r - off);
+    const uint32_t take = min(rem, k - off);
+    qn += take;
+    off += take;
+    if (off >= k || qe == kNoItem) break;  // served, or the wave already found every head dry
+    uint32_t b = kNoItem;
+    if (lane == leader) b = grab_batch(p.heads, p.n_items);
+    b = __shfl(b, (int)leader);
+    if (b == kNoItem) {  // remember it: a dry scan stalls the wave for kHeads atomics
+      qn = qe = kNoItem;
+      break;
+    }
+    qn = b;
+    qe = min(b + kQBatch, p.n_items);
+  }
+  if (lane == leader) {
+    __hip_atomic_store(wq, qn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_store(wq + 1, qe, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+  }
+  return item;
 }
 
 // A new work item for the slot: its pixel and that pixel's RNG key.
@@ -514,11 +588,12 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
     dst[1] = s.acc.y;
     dst[2] = s.acc.z;
     s.acc = mkv(R(0), R(0), R(0));
-    if (s.item + p.P >= p.n_items) {
+    const uint32_t nx = p.persist == 2 ? next_item_dyn(p) : (s.item + p.P < p.n_items ? s.item + p.P : kNoItem);
+    if (nx == kNoItem) {
       s.bounce = -1;
       return false;
     }
-    begin_item(p, s, s.item + p.P);
+    begin_item(p, s, nx);
   }
   begin_sample<R, CAMX>(p, s);
   return true;
@@ -652,11 +727,12 @@ __device__ __forceinline__ void step_body(const Params<R>& p) {
 }
 
 // Persistent form of the same loop (the default schedule): the grid is what the chip holds
-// resident, every lane keeps its path state in registers for the whole render and walks the
-// items lane, lane + P, lane + 2P, ... (P = grid lanes; shade's path regeneration does the
-// striding, as for a k_step slot). No state goes through HBM between segments, there is no
-// launch per K segments, no live-slot compaction and no shared work counter (one counter for
-// the whole chip serialises across the 8 XCDs' L2s: measured 6x slower on C2).
+// resident, every lane keeps its path state in registers for the whole render. Dynamic
+// (persist 2): shade's path regeneration pulls the next item from the wave's queue, refilled a
+// batch at a time from the per-XCD heads (one returning atomic per 64 items; per-lane atomics on
+// one counter for the whole chip serialised across the 8 XCDs' L2s: measured 6x slower on C2).
+// Static (persist 1): lanes walk items lane, lane + P, ... (P = grid lanes). No state goes
+// through HBM between segments, there is no launch per K segments and no live-slot compaction.
 template <class R, class Trav, bool CAMX>
 __device__ __forceinline__ void persist_body(const Params<R>& p) {
   __shared__ Lds<Trav::kStack * kBlock> stk;
@@ -666,7 +742,14 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
     for (uint32_t j = threadIdx.x; j < p.sc.n_nodes; j += kBlock) lds_nodes[j] = p.sc.nodes[j];
     __syncthreads();
   }
-  const uint32_t item0 = blockIdx.x * kBlock + threadIdx.x;
+  uint32_t item0 = blockIdx.x * kBlock + threadIdx.x;
+  if (p.persist == 2) {
+    if ((threadIdx.x & 63) == 0) {
+      __hip_atomic_store(wave_queue(), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      __hip_atomic_store(wave_queue() + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+    item0 = next_item_dyn(p);
+  }
   uint64_t segs = 0;
   if (item0 < p.n_items) {
     Path<R> s;
@@ -858,7 +941,7 @@ struct rt_context {
   CompiledScene scene;
   bool has_scene = false;
   DevBuf scene32, scene64;
-  DevBuf state, partial, pixmap, queue0, queue1, blk, out_tmp, counters, camx;
+  DevBuf state, partial, pixmap, queue0, queue1, blk, out_tmp, counters, camx, heads;
   CamDev cam_host;  // source of camx (kept alive for the async copy)
   uint32_t* total_host = nullptr;  // pinned
   uint64_t samples = 0;
@@ -961,7 +1044,22 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
 
 template <class KernelT, class R>
 void launch_one(KernelT kern, Params<R> p, uint32_t grid, hipStream_t st) {
-  if (p.persist) {  // the lanes stride over the items by the grid's lane count
+  if (p.persist == 2) {  // as many blocks as the chip holds resident; lanes pull items
+    static int per_cu = -1, ncu = 0;
+    if (per_cu < 0) {
+      int dev = 0, n = 0, b = 0;
+      if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) ==
+          hipSuccess && hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, kBlock, 0) == hipSuccess && b > 0) {
+        ncu = n;
+        per_cu = b;
+      } else {
+        per_cu = 0;  // unknown: keep the host's grid
+      }
+    }
+    if (per_cu > 0) grid = std::min<uint32_t>(grid, (uint32_t)(per_cu * ncu));
+    p.P = grid * kBlock;
+    p.seg_cap = (uint64_t)p.n_items * p.chunk * (uint64_t)p.max_depth + 1;
+  } else if (p.persist) {  // the lanes stride over the items by the grid's lane count
     p.P = grid * kBlock;
     p.seg_cap = ((uint64_t)p.n_items + p.P - 1) / p.P * p.chunk * (uint64_t)p.max_depth + 1;
   }
@@ -1117,8 +1215,11 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
       // one launch of P lanes (pool_slots, or kAutoPersistLanes)
       uint32_t* ctr = (uint32_t*)c->blk.ptr;
       RT_HIP(c, hipMemsetAsync(ctr, 0, 8, st));
-      p.persist = 1;
+      p.persist = RT_PERSIST_MODE;
       p.fault = ctr + 1;
+      if ((s = ensure(c, c->heads, 4ull * kHeads * kHeadStride)) != RT_OK) return s;
+      RT_HIP(c, hipMemsetAsync(c->heads.ptr, 0, 4ull * kHeads * kHeadStride, st));
+      p.heads = (uint32_t*)c->heads.ptr;
       const uint32_t grid = nblk_max;
       hipEvent_t e0 = nullptr, e1 = nullptr;
       if (c->timing) {
@@ -1267,7 +1368,7 @@ void rt_context_destroy(rt_context* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->scene32, &c->scene64, &c->state, &c->partial, &c->pixmap, &c->queue0, &c->queue1, &c->blk,
-                    &c->out_tmp, &c->counters, &c->camx})
+                    &c->out_tmp, &c->counters, &c->camx, &c->heads})
     if (b->ptr) (void)hipFree(b->ptr);
   for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
   if (c->total_host) (void)hipHostFree(c->total_host);

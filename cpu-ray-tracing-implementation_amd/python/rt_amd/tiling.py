@@ -1,9 +1,9 @@
-"""Framebuffer partitioning across ranks: 64x64 tiles dealt
+"""Framebuffer partitioning across ranks: 32x32 tiles dealt
 round-robin, each rank renders its tiles packed in order, rank 0 gathers the
 equal-size padded buffers and scatters them into the full framebuffer."""
 import numpy as np
 
-TILE = 64
+TILE = 32
 
 
 def all_tiles(w, h, ts=TILE):
