@@ -890,6 +890,23 @@ __global__ void k_zero(R* out, uint64_t n) {
   if (i < n) out[i] = R(0);
 }
 
+// The pixel map (tiles packed in order, row-major inside each tile, camera.h:154-158's pixel
+// loop per tile) built on the device from the tile list: tl[t] = {x0, y0, width, first packed
+// pixel}; pixel i belongs to the last tile whose first pixel is <= i.
+__global__ __launch_bounds__(kBlock) void k_pixmap(const uint4* tl, uint32_t ntiles, uint32_t npix, uint32_t* pixmap) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= npix) return;
+  uint32_t lo = 0, hi = ntiles - 1;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    if (tl[mid].w <= i) lo = mid;
+    else hi = mid - 1;
+  }
+  const uint4 t = tl[lo];
+  const uint32_t k = i - t.w, y = k / t.z, x = k - y * t.z;
+  pixmap[i] = (t.x + x) | (t.y + y) << 16;
+}
+
 // camera.h:137-141, 246, 253, 278-279 evaluated in double exactly as the reference orders them
 CamDev make_view(const rt_camera_desc* c) {
   CamDev v{};
@@ -941,9 +958,9 @@ struct rt_context {
   CompiledScene scene;
   bool has_scene = false;
   DevBuf scene32, scene64;
-  DevBuf state, partial, pixmap, queue0, queue1, blk, out_tmp, counters, camx, heads;
+  DevBuf state, partial, pixmap, queue0, queue1, blk, out_tmp, counters, camx, heads, tiles;
   CamDev cam_host;  // source of camx (kept alive for the async copy)
-  uint32_t* total_host = nullptr;  // pinned
+  uint32_t* total_host = nullptr;  // pinned: [0] live slots, [1] fault word, [16..] segment counter shards
   uint64_t samples = 0;
   rt_counters last{};
   int timing = 0;
@@ -1126,13 +1143,17 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
   auto t0 = std::chrono::steady_clock::now();
   rt_counters last{};
 
-  // pixel map: tiles packed in order, row-major inside each tile
-  std::vector<uint32_t> pix;
-  for (int t = 0; t < ntiles; t++)
-    for (int y = 0; y < tiles[t].height; y++)
-      for (int x = 0; x < tiles[t].width; x++)
-        pix.push_back((uint32_t)(tiles[t].x0 + x) | (uint32_t)(tiles[t].y0 + y) << 16);
-  const uint32_t npix = (uint32_t)pix.size();
+  // pixel map: tiles packed in order, row-major inside each tile (expanded by k_pixmap)
+  std::vector<uint4> tl;
+  tl.reserve(ntiles);
+  uint64_t npix64 = 0;
+  for (int t = 0; t < ntiles; t++) {
+    if (tiles[t].width == 0 || tiles[t].height == 0) continue;
+    tl.push_back(make_uint4((uint32_t)tiles[t].x0, (uint32_t)tiles[t].y0, (uint32_t)tiles[t].width, (uint32_t)npix64));
+    npix64 += (uint64_t)tiles[t].width * (uint64_t)tiles[t].height;
+  }
+  if (npix64 >= (1ull << 31)) return set_err(c, RT_ERR_INVALID_ARGUMENT, "too many pixels in one call");
+  const uint32_t npix = (uint32_t)npix64;
   if (npix == 0) return RT_OK;
   const size_t out_elems = 3ull * npix;
   rt_status s;
@@ -1173,7 +1194,10 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     if ((s = ensure(c, c->partial, 3ull * n_items * sizeof(R))) != RT_OK) return s;
     if ((s = ensure(c, c->pixmap, 4ull * npix)) != RT_OK) return s;
     if ((s = ensure(c, c->blk, 4ull * (nblk_max + 2))) != RT_OK) return s;
-    RT_HIP(c, hipMemcpyAsync(c->pixmap.ptr, pix.data(), 4ull * npix, hipMemcpyHostToDevice, st));
+    if ((s = ensure(c, c->tiles, sizeof(uint4) * tl.size())) != RT_OK) return s;
+    RT_HIP(c, hipMemcpyAsync(c->tiles.ptr, tl.data(), sizeof(uint4) * tl.size(), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_pixmap, dim3((npix + kBlock - 1) / kBlock), dim3(kBlock), 0, st, (const uint4*)c->tiles.ptr,
+                       (uint32_t)tl.size(), npix, (uint32_t*)c->pixmap.ptr);
     RT_HIP(c, hipMemsetAsync(c->counters.ptr, 0, sizeof(unsigned long long) * kSegShards, st));
 
     unsigned char* sp = (unsigned char*)c->state.ptr;
@@ -1211,6 +1235,7 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     p.K = K;
     uint64_t launches = 0, iters = 0;
     size_t ev = 0;
+    const uint32_t* fault_dev = nullptr;
     if (persist) {
       // one launch of P lanes (pool_slots, or kAutoPersistLanes)
       uint32_t* ctr = (uint32_t*)c->blk.ptr;
@@ -1235,9 +1260,7 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
         ev = 2;
       }
       launches = iters = 1;
-      RT_HIP(c, hipMemcpyAsync(c->total_host, ctr + 1, 4, hipMemcpyDeviceToHost, st));
-      RT_HIP(c, hipStreamSynchronize(st));
-      if (*c->total_host) return set_err(c, RT_ERR_HIP, "a path did not finish (internal error)");
+      fault_dev = ctr + 1;  // read back with the counters, after the resolve
     } else {
     if (p.cam_mode != RT_CAM_PERSPECTIVE || p.sc.has_procedural)
       hipLaunchKernelGGL((k_init<R, true>), dim3(nblk_max), dim3(kBlock), 0, st, p);
@@ -1292,10 +1315,14 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
                        (const R*)c->partial.ptr, npix, nchunks, spp, (R*)dout);
     launches++;
     RT_HIP(c, hipGetLastError());
-    // counters
-    unsigned long long shards[kSegShards];
-    RT_HIP(c, hipMemcpyAsync(shards, c->counters.ptr, sizeof shards, hipMemcpyDeviceToHost, st));
+    // counters (and the persistent kernel's fault word) into pinned memory: one sync per call
+    unsigned long long* shards = (unsigned long long*)(c->total_host + 16);
+    RT_HIP(c, hipMemcpyAsync(shards, c->counters.ptr, sizeof(unsigned long long) * kSegShards, hipMemcpyDeviceToHost,
+                             st));
+    if (fault_dev) RT_HIP(c, hipMemcpyAsync(c->total_host + 1, fault_dev, 4, hipMemcpyDeviceToHost, st));
+    if (!out_dev) RT_HIP(c, hipMemcpyAsync(out, dout, out_elems * sizeof(R), hipMemcpyDeviceToHost, st));
     RT_HIP(c, hipStreamSynchronize(st));
+    if (fault_dev && c->total_host[1]) return set_err(c, RT_ERR_HIP, "a path did not finish (internal error)");
     uint64_t segs = 0;
     for (int k = 0; k < kSegShards; k++) segs += shards[k];
     last.segments = segs;
@@ -1312,10 +1339,10 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
       last.step_ms = ms;
     }
   }
-  if (!out_dev) {
-    RT_HIP(c, hipMemcpyAsync(out, dout, out_elems * sizeof(R), hipMemcpyDeviceToHost, st));
+  if (prm->max_depth <= 0) {  // the rendering branch above has already synchronised
+    if (!out_dev) RT_HIP(c, hipMemcpyAsync(out, dout, out_elems * sizeof(R), hipMemcpyDeviceToHost, st));
+    RT_HIP(c, hipStreamSynchronize(st));
   }
-  RT_HIP(c, hipStreamSynchronize(st));
   last.last_render_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   uint64_t seg_total = c->last.segments + last.segments, smp_total = c->last.samples + last.samples;
   c->last = last;
@@ -1349,7 +1376,7 @@ rt_status rt_context_create(int32_t device, rt_context** out) {
     delete c;
     return set_err(nullptr, RT_ERR_HIP, hipGetErrorString(e));
   }
-  if ((e = hipHostMalloc((void**)&c->total_host, 64, hipHostMallocDefault)) != hipSuccess) {
+  if ((e = hipHostMalloc((void**)&c->total_host, 64 + 8 * kSegShards, hipHostMallocDefault)) != hipSuccess) {
     (void)hipStreamDestroy(c->stream);
     delete c;
     return set_err(nullptr, RT_ERR_HIP, hipGetErrorString(e));
@@ -1368,7 +1395,7 @@ void rt_context_destroy(rt_context* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->scene32, &c->scene64, &c->state, &c->partial, &c->pixmap, &c->queue0, &c->queue1, &c->blk,
-                    &c->out_tmp, &c->counters, &c->camx, &c->heads})
+                    &c->out_tmp, &c->counters, &c->camx, &c->heads, &c->tiles})
     if (b->ptr) (void)hipFree(b->ptr);
   for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
   if (c->total_host) (void)hipHostFree(c->total_host);
