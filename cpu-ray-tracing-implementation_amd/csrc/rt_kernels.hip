@@ -618,7 +618,7 @@ struct LinearTrav {
 };
 // The flat program (fp32, quad/box scenes such as every Cornell config): rt_device.h trace_flat.
 #ifndef RT_FLAT_WAVES
-#define RT_FLAT_WAVES 6
+#define RT_FLAT_WAVES 7
 #endif
 struct FlatTrav {
   static constexpr int kStack = 0;
