@@ -164,23 +164,18 @@ def main():
         step()
     ctx.set_timing(args.kernel_timing == "on")
     ctx.reset_counters()
-    step_ms = 0.0
-    iters = 0
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
-        st = ctx.stats()
-        step_ms += st.step_ms
-        iters += st.iterations
+        step()  # stream-ordered: the host enqueues the next frame while the GPU renders this one
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    st = ctx.stats()
-    segs = st.segments
+    st = ctx.stats()  # totals over the timed steps (kernel time from HIP events on the render stream)
+    segs, step_ms, iters = st.segments, st.step_ms, st.iterations
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -962,9 +962,20 @@ struct rt_context {
   CamDev cam_host;  // source of camx (kept alive for the async copy)
   uint32_t* total_host = nullptr;  // pinned: [0] live slots, [1] fault word, [16..] segment counter shards
   uint64_t samples = 0;
-  rt_counters last{};
+  rt_counters last{};  // host-known totals since rt_reset_counters; segments and step_ms settle in settle()
   int timing = 0;
   std::vector<hipEvent_t> events;
+  // asynchronous renders (device output): what rt_stats / rt_reset_counters / a host-output render
+  // settle with one sync -- the stream, the timing events recorded since the last settle
+  hipStream_t pend_stream = nullptr;
+  bool pending = false;
+  size_t ev_used = 0;
+  DevBuf fault;  // sticky internal-error word of the persistent kernel (zeroed by rt_reset_counters)
+  // inputs kept on the device while they do not change between calls
+  std::vector<uint4> tiles_dev;  // the tile list k_pixmap last expanded into pixmap
+  void* pixmap_for = nullptr;    // pixmap buffer that expansion went to
+  CamDev cam_dev{};              // the camera view in camx
+  bool cam_valid = false;
 };
 
 namespace {
@@ -1016,6 +1027,31 @@ hipEvent_t take_event(rt_context* c, size_t idx) {
     c->events.push_back(e);
   }
   return c->events[idx];
+}
+
+// Wait for the context's outstanding renders and fold their device-side results into c->last:
+// the cumulative segment count, the kernel time of the timing events, the fault word.
+rt_status settle(rt_context* c) {
+  if (!c->pending) return RT_OK;
+  c->pending = false;
+  RT_HIP(c, hipStreamSynchronize(c->pend_stream));
+  unsigned long long* shards = (unsigned long long*)(c->total_host + 16);
+  RT_HIP(c, hipMemcpy(shards, c->counters.ptr, sizeof(unsigned long long) * kSegShards, hipMemcpyDeviceToHost));
+  uint64_t segs = 0;
+  for (int k = 0; k < kSegShards; k++) segs += shards[k];
+  c->last.segments = segs;
+  double ms = 0;
+  for (size_t k = 0; k + 1 < c->ev_used; k += 2) {
+    float a = 0;
+    RT_HIP(c, hipEventElapsedTime(&a, c->events[k], c->events[k + 1]));
+    ms += a;
+  }
+  c->ev_used = 0;
+  c->last.step_ms += ms;
+  uint32_t fault = 0;
+  if (c->fault.ptr) RT_HIP(c, hipMemcpy(&fault, c->fault.ptr, 4, hipMemcpyDeviceToHost));
+  if (fault) return set_err(c, RT_ERR_HIP, "a path did not finish (internal error)");
+  return RT_OK;
 }
 
 // Division by a launch constant d >= 1 as a multiply (Granlund-Montgomery): with
@@ -1141,7 +1177,6 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
   const SceneHeader& hdr = f64 ? cs.hdr64 : cs.hdr;
   void* sbase = f64 ? c->scene64.ptr : c->scene32.ptr;
   auto t0 = std::chrono::steady_clock::now();
-  rt_counters last{};
 
   // pixel map: tiles packed in order, row-major inside each tile (expanded by k_pixmap)
   std::vector<uint4> tl;
@@ -1192,13 +1227,20 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
       if ((s = ensure(c, c->queue1, 4ull * P)) != RT_OK) return s;
     }
     if ((s = ensure(c, c->partial, 3ull * n_items * sizeof(R))) != RT_OK) return s;
+    const size_t pixmap_bytes = c->pixmap.bytes;
     if ((s = ensure(c, c->pixmap, 4ull * npix)) != RT_OK) return s;
+    if (c->pixmap.bytes != pixmap_bytes) c->tiles_dev.clear();  // reallocated: the old map is gone
     if ((s = ensure(c, c->blk, 4ull * (nblk_max + 2))) != RT_OK) return s;
-    if ((s = ensure(c, c->tiles, sizeof(uint4) * tl.size())) != RT_OK) return s;
-    RT_HIP(c, hipMemcpyAsync(c->tiles.ptr, tl.data(), sizeof(uint4) * tl.size(), hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_pixmap, dim3((npix + kBlock - 1) / kBlock), dim3(kBlock), 0, st, (const uint4*)c->tiles.ptr,
-                       (uint32_t)tl.size(), npix, (uint32_t*)c->pixmap.ptr);
-    RT_HIP(c, hipMemsetAsync(c->counters.ptr, 0, sizeof(unsigned long long) * kSegShards, st));
+    const bool same_tiles = c->pixmap_for == c->pixmap.ptr && c->tiles_dev.size() == tl.size() &&
+                            std::memcmp(c->tiles_dev.data(), tl.data(), sizeof(uint4) * tl.size()) == 0;
+    if (!same_tiles) {  // the pixel map of an unchanged tile list is still in pixmap
+      if ((s = ensure(c, c->tiles, sizeof(uint4) * tl.size())) != RT_OK) return s;
+      RT_HIP(c, hipMemcpyAsync(c->tiles.ptr, tl.data(), sizeof(uint4) * tl.size(), hipMemcpyHostToDevice, st));
+      hipLaunchKernelGGL(k_pixmap, dim3((npix + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
+                         (const uint4*)c->tiles.ptr, (uint32_t)tl.size(), npix, (uint32_t*)c->pixmap.ptr);
+      c->tiles_dev = tl;
+      c->pixmap_for = c->pixmap.ptr;
+    }
 
     unsigned char* sp = (unsigned char*)c->state.ptr;
     Params<R> p{};
@@ -1227,7 +1269,11 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     p.seed = prm->seed;
     c->cam_host = make_view(cam);
     if ((s = ensure(c, c->camx, sizeof(CamDev))) != RT_OK) return s;
-    RT_HIP(c, hipMemcpyAsync(c->camx.ptr, &c->cam_host, sizeof(CamDev), hipMemcpyHostToDevice, st));
+    if (!c->cam_valid || std::memcmp(&c->cam_dev, &c->cam_host, sizeof(CamDev)) != 0) {
+      RT_HIP(c, hipMemcpyAsync(c->camx.ptr, &c->cam_host, sizeof(CamDev), hipMemcpyHostToDevice, st));
+      c->cam_dev = c->cam_host;
+      c->cam_valid = true;
+    }
     p.cam_mode = c->cam_host.mode;
     p.camx = (const CamDev*)c->camx.ptr;
     p.seg_shards = (unsigned long long*)c->counters.ptr;
@@ -1235,21 +1281,22 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     p.K = K;
     uint64_t launches = 0, iters = 0;
     size_t ev = 0;
-    const uint32_t* fault_dev = nullptr;
+    if (c->timing && c->ev_used > 4096 && (s = settle(c)) != RT_OK) return s;  // bound the pending events
+    if (c->pending && c->pend_stream != st) RT_HIP(c, hipStreamSynchronize(c->pend_stream));  // one stream pending
+    const size_t ev0 = c->ev_used;
     if (persist) {
       // one launch of P lanes (pool_slots, or kAutoPersistLanes)
-      uint32_t* ctr = (uint32_t*)c->blk.ptr;
-      RT_HIP(c, hipMemsetAsync(ctr, 0, 8, st));
+      if ((s = ensure(c, c->fault, 4)) != RT_OK) return s;
       p.persist = RT_PERSIST_MODE;
-      p.fault = ctr + 1;
+      p.fault = (uint32_t*)c->fault.ptr;
       if ((s = ensure(c, c->heads, 4ull * kHeads * kHeadStride)) != RT_OK) return s;
       RT_HIP(c, hipMemsetAsync(c->heads.ptr, 0, 4ull * kHeads * kHeadStride, st));
       p.heads = (uint32_t*)c->heads.ptr;
       const uint32_t grid = nblk_max;
       hipEvent_t e0 = nullptr, e1 = nullptr;
       if (c->timing) {
-        e0 = take_event(c, 0);
-        e1 = take_event(c, 1);
+        e0 = take_event(c, ev0);
+        e1 = take_event(c, ev0 + 1);
         if (!e0 || !e1) return set_err(c, RT_ERR_HIP, "hipEventCreate failed");
         RT_HIP(c, hipEventRecord(e0, st));
       }
@@ -1260,7 +1307,7 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
         ev = 2;
       }
       launches = iters = 1;
-      fault_dev = ctr + 1;  // read back with the counters, after the resolve
+      // a fault is reported by the settle after this call (rt_stats, or a host-output render)
     } else {
     if (p.cam_mode != RT_CAM_PERSPECTIVE || p.sc.has_procedural)
       hipLaunchKernelGGL((k_init<R, true>), dim3(nblk_max), dim3(kBlock), 0, st, p);
@@ -1279,7 +1326,7 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
       const uint32_t grid = (p.n + kBlock - 1) / kBlock;
       for (int b = 0; b < kBatch; b++) {
         if (c->timing) {
-          hipEvent_t e0 = take_event(c, ev), e1 = take_event(c, ev + 1);
+          hipEvent_t e0 = take_event(c, ev0 + ev), e1 = take_event(c, ev0 + ev + 1);
           if (!e0 || !e1) return set_err(c, RT_ERR_HIP, "hipEventCreate failed");
           RT_HIP(c, hipEventRecord(e0, st));
           launch_step<R>(p, cs.stack_need, hdr.n_spheres > 0, hdr.n_tris > 0, grid, st);
@@ -1315,39 +1362,21 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
                        (const R*)c->partial.ptr, npix, nchunks, spp, (R*)dout);
     launches++;
     RT_HIP(c, hipGetLastError());
-    // counters (and the persistent kernel's fault word) into pinned memory: one sync per call
-    unsigned long long* shards = (unsigned long long*)(c->total_host + 16);
-    RT_HIP(c, hipMemcpyAsync(shards, c->counters.ptr, sizeof(unsigned long long) * kSegShards, hipMemcpyDeviceToHost,
-                             st));
-    if (fault_dev) RT_HIP(c, hipMemcpyAsync(c->total_host + 1, fault_dev, 4, hipMemcpyDeviceToHost, st));
-    if (!out_dev) RT_HIP(c, hipMemcpyAsync(out, dout, out_elems * sizeof(R), hipMemcpyDeviceToHost, st));
-    RT_HIP(c, hipStreamSynchronize(st));
-    if (fault_dev && c->total_host[1]) return set_err(c, RT_ERR_HIP, "a path did not finish (internal error)");
-    uint64_t segs = 0;
-    for (int k = 0; k < kSegShards; k++) segs += shards[k];
-    last.segments = segs;
-    last.samples = (uint64_t)npix * spp;
-    last.iterations = iters;
-    last.launches = launches;
-    if (c->timing) {
-      double ms = 0;
-      for (size_t k = 0; k + 1 < ev; k += 2) {
-        float a = 0;
-        RT_HIP(c, hipEventElapsedTime(&a, c->events[k], c->events[k + 1]));
-        ms += a;
-      }
-      last.step_ms = ms;
-    }
+    // device output: nothing waits here -- the segment counters (cumulative on the device), the
+    // timing events and the fault word are settled by rt_stats, rt_reset_counters or a host-output call
+    c->ev_used = ev0 + ev;
+    c->pending = true;
+    c->pend_stream = st;
+    c->last.samples += (uint64_t)npix * spp;
+    c->last.iterations += iters;
+    c->last.launches += launches;
   }
-  if (prm->max_depth <= 0) {  // the rendering branch above has already synchronised
-    if (!out_dev) RT_HIP(c, hipMemcpyAsync(out, dout, out_elems * sizeof(R), hipMemcpyDeviceToHost, st));
+  if (!out_dev) {
+    RT_HIP(c, hipMemcpyAsync(out, dout, out_elems * sizeof(R), hipMemcpyDeviceToHost, st));
     RT_HIP(c, hipStreamSynchronize(st));
+    if ((s = settle(c)) != RT_OK) return s;
   }
-  last.last_render_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  uint64_t seg_total = c->last.segments + last.segments, smp_total = c->last.samples + last.samples;
-  c->last = last;
-  c->last.segments = seg_total;  // cumulative since rt_reset_counters
-  c->last.samples = smp_total;
+  c->last.last_render_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return RT_OK;
 }
 
@@ -1381,7 +1410,9 @@ rt_status rt_context_create(int32_t device, rt_context** out) {
     delete c;
     return set_err(nullptr, RT_ERR_HIP, hipGetErrorString(e));
   }
-  if (ensure(c, c->counters, sizeof(unsigned long long) * kSegShards) != RT_OK) {
+  if (ensure(c, c->counters, sizeof(unsigned long long) * kSegShards) != RT_OK || ensure(c, c->fault, 4) != RT_OK ||
+      hipMemset(c->counters.ptr, 0, sizeof(unsigned long long) * kSegShards) != hipSuccess ||
+      hipMemset(c->fault.ptr, 0, 4) != hipSuccess) {
     std::string m = c->err;
     rt_context_destroy(c);
     return set_err(nullptr, RT_ERR_OUT_OF_MEMORY, m);
@@ -1395,7 +1426,7 @@ void rt_context_destroy(rt_context* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->scene32, &c->scene64, &c->state, &c->partial, &c->pixmap, &c->queue0, &c->queue1, &c->blk,
-                    &c->out_tmp, &c->counters, &c->camx, &c->heads, &c->tiles})
+                    &c->out_tmp, &c->counters, &c->camx, &c->heads, &c->tiles, &c->fault})
     if (b->ptr) (void)hipFree(b->ptr);
   for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
   if (c->total_host) (void)hipHostFree(c->total_host);
@@ -1484,14 +1515,21 @@ rt_status rt_render_tiles(rt_context* c, const rt_camera_desc* cam, const rt_ren
 
 rt_status rt_stats(rt_context* c, rt_counters* out) {
   if (!c || !out) return set_err(c, RT_ERR_INVALID_ARGUMENT, "null argument");
+  RT_HIP(c, hipSetDevice(c->device));
+  const rt_status s = settle(c);
   *out = c->last;
-  return RT_OK;
+  return s;
 }
 
 rt_status rt_reset_counters(rt_context* c) {
   if (!c) return set_err(nullptr, RT_ERR_INVALID_ARGUMENT, "null context");
+  RT_HIP(c, hipSetDevice(c->device));
+  const rt_status s = settle(c);
+  RT_HIP(c, hipMemset(c->counters.ptr, 0, sizeof(unsigned long long) * kSegShards));
+  if (c->fault.ptr) RT_HIP(c, hipMemset(c->fault.ptr, 0, 4));
+  RT_HIP(c, hipDeviceSynchronize());
   c->last = rt_counters{};
-  return RT_OK;
+  return s;
 }
 
 rt_status rt_set_timing(rt_context* c, int32_t enable) {

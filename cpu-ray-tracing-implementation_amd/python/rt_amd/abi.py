@@ -26,7 +26,7 @@ RT_TEX_SOLID, RT_TEX_CHECKER, RT_TEX_PERLIN, RT_TEX_VALUE, RT_TEX_WORLEY, RT_TEX
 RT_CAM_PERSPECTIVE, RT_CAM_ORTHONORMAL, RT_CAM_FISHEYE, RT_CAM_LENS = range(4)
 RT_PREC_F32, RT_PREC_F64 = 0, 1
 RT_TRAV_AUTO, RT_TRAV_ORDERED = 0, 1
-ABI_VERSION = 3  # include/rt_hip.h RT_ABI_VERSION
+ABI_VERSION = 4  # include/rt_hip.h RT_ABI_VERSION
 
 
 class rt_object(ctypes.Structure):

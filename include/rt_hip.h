@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 typedef enum rt_status {
   RT_OK = 0,
@@ -210,10 +210,10 @@ typedef struct rt_tile {
 typedef struct rt_counters {
   uint64_t segments;   /* ray segments traced (world.hit calls, camera.h:198) */
   uint64_t samples;    /* camera samples completed */
-  uint64_t iterations; /* extend/shade rounds of the last render */
-  uint64_t launches;   /* kernel launches of the last render */
-  double last_render_ms;
-  double step_ms; /* device time of the path-step kernels (last render, when timing is enabled) */
+  uint64_t iterations; /* extend/shade rounds (k_persist launches, or k_step rounds) */
+  uint64_t launches;   /* kernel launches */
+  double last_render_ms; /* host time of the last rt_render_tiles call (enqueue time when asynchronous) */
+  double step_ms; /* device time of the path-step kernels (when timing is enabled) */
   double aux_ms;  /* reserved */
 } rt_counters;
 
@@ -247,12 +247,15 @@ rt_status rt_scene_upload(rt_context* ctx, const rt_scene_desc* desc);
  * device. Returns RT_OK, RT_ERR_INVALID_ARGUMENT or RT_ERR_UNSUPPORTED (message in err). */
 rt_status rt_scene_check(const rt_scene_desc* desc, rt_scene_info* info, char* err, int32_t errlen);
 
-/* Render `ntiles` rectangles of the image described by `cam`. */
+/* Render `ntiles` rectangles of the image described by `cam`. With out_is_device = 1 the call
+ * is stream-ordered and returns without waiting for the GPU (the output is ready for later work
+ * on `stream`); a device-side failure is then reported by the next rt_stats, rt_reset_counters or
+ * host-output render. With out_is_device = 0 it returns once out_rgb holds the image. */
 rt_status rt_render_tiles(rt_context* ctx, const rt_camera_desc* cam, const rt_render_params* params,
                           const rt_tile* tiles, int32_t ntiles, void* out_rgb, int32_t out_is_device,
                           void* stream);
 
-/* Counters since the last rt_reset_counters (segments, samples) and of the last render. */
+/* Counters since the last rt_reset_counters; waits for outstanding renders of the context. */
 rt_status rt_stats(rt_context* ctx, rt_counters* out);
 rt_status rt_reset_counters(rt_context* ctx);
 

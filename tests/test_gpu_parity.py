@@ -125,6 +125,37 @@ def test_image_invariant_to_schedule_and_tiling(ctx, precision):
     assert np.array_equal(fb.reshape(base.shape), base)
 
 
+def test_async_device_output_and_cumulative_counters(ctx):
+    # device output returns without waiting (rt_hip.h rt_render_tiles); renders queued back to back on
+    # one stream equal the synchronous host-output render, and rt_stats settles the counters of all
+    import torch
+    desc, cam, _, _ = scenes.cornell_box(width=48)
+    ctx.upload(desc)
+    host = ctx.render(cam, 16, 8, seed=4, precision=F32)
+    W, H = cam.image_width, cam.image_height
+    from rt_amd.tiling import pixel_index, plan
+    tiles, counts, maxpix = plan(W, H, 2, ts=16)
+    p = ctx.params(16, 8, 4, F32)
+    outs = [torch.zeros((maxpix, 3), dtype=torch.float32, device="cuda") for _ in range(2)]
+    stream = torch.cuda.current_stream().cuda_stream
+    ctx.set_timing(True)
+    ctx.reset_counters()
+    for _ in range(3):  # the same tiles again: the device-side pixel map and camera are reused
+        for r in range(2):
+            ctx.render_tiles(cam, p, tiles[r], outs[r].data_ptr(), 1, stream)
+    st = ctx.stats()
+    ctx.set_timing(False)
+    fb = np.zeros((H * W, 3), dtype=np.float32)
+    for r in range(2):
+        fb[pixel_index(tiles[r], W)] = outs[r][: counts[r]].cpu().numpy()
+    assert np.array_equal(fb.reshape(host.shape), host)
+    assert st.samples == 3 * W * H * 16 and st.iterations == 6 and st.step_ms > 0
+    ctx.reset_counters()
+    ctx.render(cam, 16, 8, seed=4, precision=F32)
+    one = ctx.stats().segments
+    assert st.segments == 3 * one
+
+
 def test_sample_ranges_compose(ctx):
     desc, cam, _, _ = scenes.cornell_box(width=40)
     ctx.upload(desc)
