@@ -52,8 +52,11 @@ constexpr int kBlock = 256;
 #ifndef RT_PERSIST_MODE  // 2: dynamic (per-XCD heads), 1: static striding (development A/B)
 #define RT_PERSIST_MODE 2
 #endif
-#ifndef RT_STACK_WAVES
-#define RT_STACK_WAVES 3
+#ifndef RT_STACK_WAVES  // 4: the LDS limit of the LDS-node BVH kernel (32.8 KB per block); C3 151 -> 129 ms vs 3
+#define RT_STACK_WAVES 4
+#endif
+#ifndef RT_LINEAR_VOL_WAVES  // fp32 quad + volume linear program (C5): 1 (128 VGPRs, 4 waves) 3385 ms, 5: 4674, 6: 5933
+#define RT_LINEAR_VOL_WAVES 1
 #endif
 constexpr int kBatch = 16;           // extend/shade rounds between live-slot counts
 constexpr int kSegShards = 256;      // segment counter shards
@@ -608,7 +611,10 @@ struct LinearTrav {
   static constexpr int kStack = 0;
   // waves per SIMD the register budget is cut for (occupancy hides the shading loads); the
   // lean quad-only program fits 96 VGPRs with a small spill, the others would spill heavily
-  static constexpr int kWaves = (sizeof(R) == 4 && !SPH && !TRI && !VOL) ? RT_LINEAR_WAVES : 1;
+  static constexpr int kWaves = sizeof(R) != 4 ? 1
+                                 : (!SPH && !TRI && !VOL) ? RT_LINEAR_WAVES
+                                 : (!SPH && !TRI && VOL)  ? RT_LINEAR_VOL_WAVES
+                                                          : 1;
   static constexpr int kLdsNodes = 0;
   static constexpr bool kFlat = false;
   __device__ __forceinline__ static void run(const DevScene<R>& sc, const Node<R>*, const Path<R>& s, Keys k,
