@@ -8,7 +8,7 @@ ARCH     ?= gfx950
 # launch-per-K kernels (same shade code, different inlining) produce bit-identical images
 HIPFLAGS ?= -O3 -std=c++17 -fPIC -Wall -ffp-contract=on --offload-arch=$(ARCH)
 
-LIB_SRCS := $(PKG)/csrc/rt_kernels.hip $(PKG)/csrc/scene_compile.cpp
+LIB_SRCS := $(PKG)/csrc/rt_kernels.hip $(PKG)/csrc/rt_multi.hip $(PKG)/csrc/scene_compile.cpp
 LIB_HDRS := $(PKG)/csrc/rt_device.h $(PKG)/csrc/rt_sin.h $(PKG)/csrc/rt_scene.h $(PKG)/csrc/scene_compile.h include/rt_hip.h
 
 CXX      ?= g++
@@ -19,7 +19,7 @@ all: $(BUILD)/librt_hip.so $(BUILD)/librt_scenes.so $(BUILD)/rt_main oracle
 
 $(BUILD)/librt_hip.so: $(LIB_SRCS) $(LIB_HDRS)
 	@mkdir -p $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(LIB_SRCS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(LIB_SRCS) -ldl
 
 # development build with correctly rounded fp32 math (scripts/dev_divergence.py --lib)
 precise: $(BUILD)/librt_hip_precise.so

@@ -28,6 +28,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <new>
 #include <stdexcept>
@@ -1101,27 +1102,41 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
   return s;
 }
 
+// Resident blocks of one kernel on one device (occupancy query x CU count), cached per (kernel,
+// device): every persistent kernel has its own register budget, so one kernel's grid must not
+// size another's. Guarded: contexts on different host threads launch concurrently.
+std::mutex g_occ_mu;
+std::map<std::pair<const void*, int>, uint32_t> g_occ;
+
+uint32_t resident_blocks(const void* kern, int dev) {
+  std::lock_guard<std::mutex> lk(g_occ_mu);
+  auto it = g_occ.find({kern, dev});
+  if (it != g_occ.end()) return it->second;
+  int n = 0, b = 0;
+  uint32_t r = 0;  // unknown: keep the host's grid
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, kBlock, 0) == hipSuccess && b > 0 && n > 0)
+    r = (uint32_t)(b * n);
+  g_occ[{kern, dev}] = r;
+  return r;
+}
+
+// lanes of the last persistent launch on this host thread (rt_counters.grid_lanes)
+thread_local uint64_t t_grid_lanes = 0;
+
 template <class KernelT, class R>
 void launch_one(KernelT kern, Params<R> p, uint32_t grid, hipStream_t st) {
   if (p.persist == 2) {  // as many blocks as the chip holds resident; lanes pull items
-    static int per_cu = -1, ncu = 0;
-    if (per_cu < 0) {
-      int dev = 0, n = 0, b = 0;
-      if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) ==
-          hipSuccess && hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, kBlock, 0) == hipSuccess && b > 0) {
-        ncu = n;
-        per_cu = b;
-      } else {
-        per_cu = 0;  // unknown: keep the host's grid
-      }
-    }
-    if (per_cu > 0) grid = std::min<uint32_t>(grid, (uint32_t)(per_cu * ncu));
+    int dev = 0;
+    const uint32_t res = hipGetDevice(&dev) == hipSuccess ? resident_blocks((const void*)kern, dev) : 0;
+    if (res > 0) grid = std::min<uint32_t>(grid, res);
     p.P = grid * kBlock;
     p.seg_cap = (uint64_t)p.n_items * p.chunk * (uint64_t)p.max_depth + 1;
   } else if (p.persist) {  // the lanes stride over the items by the grid's lane count
     p.P = grid * kBlock;
     p.seg_cap = ((uint64_t)p.n_items + p.P - 1) / p.P * p.chunk * (uint64_t)p.max_depth + 1;
   }
+  if (p.persist) t_grid_lanes = (uint64_t)grid * kBlock;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, st, p);
 }
 template <class R, class Trav>
@@ -1183,6 +1198,9 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
   const SceneHeader& hdr = f64 ? cs.hdr64 : cs.hdr;
   void* sbase = f64 ? c->scene64.ptr : c->scene32.ptr;
   auto t0 = std::chrono::steady_clock::now();
+  // A device-output render still pending on another stream reads the context's shared buffers
+  // (pixmap, tiles, camx, heads, partial): wait for it before this call writes any of them.
+  if (c->pending && c->pend_stream != st) RT_HIP(c, hipStreamSynchronize(c->pend_stream));
 
   // pixel map: tiles packed in order, row-major inside each tile (expanded by k_pixmap)
   std::vector<uint4> tl;
@@ -1241,11 +1259,12 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
                             std::memcmp(c->tiles_dev.data(), tl.data(), sizeof(uint4) * tl.size()) == 0;
     if (!same_tiles) {  // the pixel map of an unchanged tile list is still in pixmap
       if ((s = ensure(c, c->tiles, sizeof(uint4) * tl.size())) != RT_OK) return s;
-      RT_HIP(c, hipMemcpyAsync(c->tiles.ptr, tl.data(), sizeof(uint4) * tl.size(), hipMemcpyHostToDevice, st));
+      c->tiles_dev = tl;  // the copy's source outlives this call
+      c->pixmap_for = c->pixmap.ptr;
+      RT_HIP(c, hipMemcpyAsync(c->tiles.ptr, c->tiles_dev.data(), sizeof(uint4) * tl.size(), hipMemcpyHostToDevice,
+                               st));
       hipLaunchKernelGGL(k_pixmap, dim3((npix + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
                          (const uint4*)c->tiles.ptr, (uint32_t)tl.size(), npix, (uint32_t*)c->pixmap.ptr);
-      c->tiles_dev = tl;
-      c->pixmap_for = c->pixmap.ptr;
     }
 
     unsigned char* sp = (unsigned char*)c->state.ptr;
@@ -1288,7 +1307,6 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     uint64_t launches = 0, iters = 0;
     size_t ev = 0;
     if (c->timing && c->ev_used > 4096 && (s = settle(c)) != RT_OK) return s;  // bound the pending events
-    if (c->pending && c->pend_stream != st) RT_HIP(c, hipStreamSynchronize(c->pend_stream));  // one stream pending
     const size_t ev0 = c->ev_used;
     if (persist) {
       // one launch of P lanes (pool_slots, or kAutoPersistLanes)
@@ -1308,6 +1326,7 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
       }
       launch_step<R>(p, cs.stack_need, hdr.n_spheres > 0, hdr.n_tris > 0, grid, st);
       RT_HIP(c, hipGetLastError());
+      c->last.grid_lanes = t_grid_lanes;
       if (c->timing) {
         RT_HIP(c, hipEventRecord(e1, st));
         ev = 2;
@@ -1508,7 +1527,9 @@ rt_status rt_render_tiles(rt_context* c, const rt_camera_desc* cam, const rt_ren
       return set_err(c, RT_ERR_INVALID_ARGUMENT, "tile " + std::to_string(t) + " outside the image");
   }
   RT_HIP(c, hipSetDevice(c->device));
-  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  // NULL is the HIP null stream (torch's default stream), so work the caller queues after this call
+  // on that stream -- a clone, a gather -- is ordered after the render
+  hipStream_t st = (hipStream_t)stream;
   try {
     if (prm->precision == RT_PREC_F64) return render<double>(c, cam, prm, tiles, ntiles, out_rgb, out_is_device, st);
     return render<float>(c, cam, prm, tiles, ntiles, out_rgb, out_is_device, st);

@@ -26,7 +26,7 @@ RT_TEX_SOLID, RT_TEX_CHECKER, RT_TEX_PERLIN, RT_TEX_VALUE, RT_TEX_WORLEY, RT_TEX
 RT_CAM_PERSPECTIVE, RT_CAM_ORTHONORMAL, RT_CAM_FISHEYE, RT_CAM_LENS = range(4)
 RT_PREC_F32, RT_PREC_F64 = 0, 1
 RT_TRAV_AUTO, RT_TRAV_ORDERED = 0, 1
-ABI_VERSION = 4  # include/rt_hip.h RT_ABI_VERSION
+ABI_VERSION = 5  # include/rt_hip.h RT_ABI_VERSION
 
 
 class rt_object(ctypes.Structure):
@@ -73,7 +73,8 @@ class rt_tile(ctypes.Structure):
 
 class rt_counters(ctypes.Structure):
     _fields_ = [("segments", c_uint64), ("samples", c_uint64), ("iterations", c_uint64), ("launches", c_uint64),
-                ("last_render_ms", c_double), ("step_ms", c_double), ("aux_ms", c_double)]
+                ("last_render_ms", c_double), ("step_ms", c_double), ("aux_ms", c_double),
+                ("grid_lanes", c_uint64)]
 
 
 class rt_scene_info(ctypes.Structure):
@@ -97,6 +98,15 @@ SIGNATURES = {
     "rt_reset_counters": (c_int32, [ctypes.c_void_p]),
     "rt_set_timing": (c_int32, [ctypes.c_void_p, c_int32]),
     "rt_rng_u32": (c_uint32, [c_uint64, c_uint32, c_uint32, c_uint32]),
+    "rt_multi_create": (c_int32, [ctypes.POINTER(c_int32), c_int32, ctypes.POINTER(ctypes.c_void_p)]),
+    "rt_multi_destroy": (None, [ctypes.c_void_p]),
+    "rt_multi_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
+    "rt_multi_uses_rccl": (c_int32, [ctypes.c_void_p]),
+    "rt_multi_scene_upload": (c_int32, [ctypes.c_void_p, ctypes.POINTER(rt_scene_desc)]),
+    "rt_multi_render": (c_int32, [ctypes.c_void_p, ctypes.POINTER(rt_camera_desc), ctypes.POINTER(rt_render_params),
+                                  c_int32, ctypes.c_void_p]),
+    "rt_multi_stats": (c_int32, [ctypes.c_void_p, c_int32, ctypes.POINTER(rt_counters)]),
+    "rt_multi_plan": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int32, ctypes.POINTER(rt_tile), c_int32]),
 }
 
 _lib = None

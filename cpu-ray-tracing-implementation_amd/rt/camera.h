@@ -100,14 +100,11 @@ class camera {
     }
     rt_scene_desc desc = sb.desc(w, l, bg);
     rt_camera_desc cam = describe();
-    rt_context* ctx = nullptr;
-    if (rt_context_create(device_, &ctx) != RT_OK) return fail(rt_last_error(nullptr));
     rt_render_params p{};
     p.spp = samples_per_pixel_;
     p.max_depth = max_recur_depth_;
     p.seed = seed_;
     p.precision = precision_;
-    rt_tile tile{0, 0, image_width_, image_height_};
     const size_t n = (size_t)image_width_ * image_height_;
     std::vector<double> px64;
     std::vector<float> px32;
@@ -119,14 +116,31 @@ class camera {
       px32.resize(3 * n);
       out = px32.data();
     }
-    rt_status s = rt_scene_upload(ctx, &desc);
-    if (s == RT_OK) s = rt_render_tiles(ctx, &cam, &p, &tile, 1, out, 0, nullptr);
-    if (s != RT_OK) {
-      std::string m = rt_last_error(ctx);
+    if (!devices_.empty()) {  // the image tiled over several GPUs, one RCCL gather (rt_multi_*)
+      rt_multi* mg = nullptr;
+      if (rt_multi_create(devices_.data(), (int32_t)devices_.size(), &mg) != RT_OK)
+        return fail(rt_multi_last_error(nullptr));
+      rt_status s = rt_multi_scene_upload(mg, &desc);
+      if (s == RT_OK) s = rt_multi_render(mg, &cam, &p, tile_size_, out);
+      if (s != RT_OK) {
+        std::string m = rt_multi_last_error(mg);
+        rt_multi_destroy(mg);
+        return fail(m);
+      }
+      rt_multi_destroy(mg);
+    } else {
+      rt_context* ctx = nullptr;
+      if (rt_context_create(device_, &ctx) != RT_OK) return fail(rt_last_error(nullptr));
+      rt_tile tile{0, 0, image_width_, image_height_};
+      rt_status s = rt_scene_upload(ctx, &desc);
+      if (s == RT_OK) s = rt_render_tiles(ctx, &cam, &p, &tile, 1, out, 0, nullptr);
+      if (s != RT_OK) {
+        std::string m = rt_last_error(ctx);
+        rt_context_destroy(ctx);
+        return fail(m);
+      }
       rt_context_destroy(ctx);
-      return fail(m);
     }
-    rt_context_destroy(ctx);
     image_.resize(n);
     for (size_t i = 0; i < n; i++)
       image_[i] = precision_ == RT_PREC_F64 ? color(px64[3 * i], px64[3 * i + 1], px64[3 * i + 2])
@@ -187,6 +201,10 @@ class camera {
   std::shared_ptr<texture> background_;
   // device-path settings (not in the reference)
   int device_ = 0;                      // HIP device
+  // non-empty: render on these devices, tiles of tile_size_ dealt round-robin and gathered over RCCL
+  // to devices_[0] (rt_multi_*; replaces camera.h:154-172's per-row par_unseq)
+  std::vector<int32_t> devices_;
+  int tile_size_ = 32;
   rt_precision precision_ = RT_PREC_F32;  // RT_PREC_F64: the fp64 parity path
   uint64_t seed_ = 1;                   // counter-RNG key
   std::string last_error_;

@@ -259,6 +259,22 @@ void sponza(int width, double aspect, config_scene* s) {
                                 5);
 }
 
+// main.cc:345-400: the Fox glTF (576 non-indexed float triangles) as glass triangles under a BVH,
+// the bathroom.exr skybox (absent from the reference's checkout: the picture texture samples
+// magenta, image.h:25,75-76), no importance-sampled light.
+void glass_fox(int width, double aspect, config_scene* s) {
+  gltf::GltfLoader model(asset("Fox/glTF/Fox.gltf").c_str());
+  auto skybox = std::make_shared<picture_texture>(std::make_shared<image>(asset("bathroom.exr").c_str()));
+  hittable_list world;
+  for (const auto& t : gltf_triangles(model.getOutputPrimitives()))
+    world.push_back(std::make_shared<triangle>(
+        t[0], t[1], t[2], std::make_shared<dielectric>(std::make_shared<solid_color>(color(1.0f)), 1.5)));
+  s->world = std::make_shared<bvh_node>(world);
+  s->cam.initialize_perspective(W(width, 600), A(aspect, 1.0), point3(220, 220, 220), point3(0, 20, 0), 1, 45.0, 200,
+                                5);
+  s->cam.background_ = skybox;
+}
+
 }  // namespace
 
 bool build_config_scene(const std::string& name, int width, double aspect, config_scene* out) {
@@ -274,6 +290,8 @@ bool build_config_scene(const std::string& name, int width, double aspect, confi
     three_material_ball_with_defocus_blur(width, aspect, out);
   else if (name == "sponza")
     sponza(width, aspect, out);
+  else if (name == "glass_fox")
+    glass_fox(width, aspect, out);
   else if (name == "skybox_and_fisheye")
     skybox_and_fisheye(width, aspect, out);
   else if (name == "skybox_and_motion_blur")
@@ -349,10 +367,12 @@ long long rtsc_gltf_triangles(const char* path, double* xyz, long long cap, char
   }
 }
 
-// The full drop-in path: build the scene, camera::render(of, world, light) to a PPM file.
-int rtsc_render_ppm(const char* name, int width, double aspect, int spp, int max_depth, uint64_t seed, int precision,
-                    const char* path, char* err, int errlen) {
+// The full drop-in path: build the scene, camera::render(of, world, light) to a PPM file; with
+// ndev > 0 the camera renders on `devices` (camera::devices_, the rt_multi_* tiling + RCCL gather).
+int rtsc_render_ppm_on(const char* name, int width, double aspect, int spp, int max_depth, uint64_t seed,
+                       int precision, const int32_t* devices, int ndev, const char* path, char* err, int errlen) {
   config_scene s;
+  if (devices && ndev > 0) s.cam.devices_.assign(devices, devices + ndev);
   if (!name || !build_config_scene(name, width, aspect, &s)) {
     if (err && errlen > 0) std::snprintf(err, (size_t)errlen, "unknown scene");
     return 1;
@@ -368,6 +388,11 @@ int rtsc_render_ppm(const char* name, int width, double aspect, int spp, int max
     return 2;
   }
   return 0;
+}
+
+int rtsc_render_ppm(const char* name, int width, double aspect, int spp, int max_depth, uint64_t seed, int precision,
+                    const char* path, char* err, int errlen) {
+  return rtsc_render_ppm_on(name, width, aspect, spp, max_depth, seed, precision, nullptr, 0, path, err, errlen);
 }
 
 }  // extern "C"

@@ -20,7 +20,8 @@ struct config_scene {
 };
 
 // name: cornell_box | cornell_box_with_volume | rtow | rtow_motion | three_material_ball |
-// three_material_ball_with_defocus_blur | sponza ($RT_SPONZA_GLTF or ./assets/Sponza/glTF/Sponza.gltf).
+// three_material_ball_with_defocus_blur | sponza ($RT_SPONZA_GLTF or ./assets/Sponza/glTF/Sponza.gltf) |
+// glass_fox ($RT_ASSETS/Fox/glTF/Fox.gltf) | the skybox and noise scenes.
 // width/aspect <= 0 keep the scene's own camera. Returns false for an unknown name; throws
 // std::runtime_error when a scene's asset cannot be loaded.
 bool build_config_scene(const std::string& name, int width, double aspect, config_scene* out);

@@ -24,8 +24,14 @@
  *  - One rt_context per HIP device. A context is not re-entrant; different
  *    contexts may be used from different host threads concurrently.
  *  - rt_render_tiles is stream-ordered on the caller's stream (hipStream_t
- *    passed as void*, NULL = the context's own stream) when out_rgb is a
- *    device pointer; with a host pointer it returns after the copy.
+ *    passed as void*; NULL = the HIP null stream, which is also torch's
+ *    default stream) when out_rgb is a device pointer: work queued on that
+ *    stream after the call sees the finished image. With a host pointer it
+ *    returns after the copy.
+ *  - rt_multi_* drive several devices from one process (camera.h:154-172's
+ *    row parallelism lifted to tiles over GPUs): one
+ *    context per device and one RCCL communicator (ncclCommInitAll) whose
+ *    ncclGather brings every device's tiles to the first device.
  *  - All geometry in the descriptor is double precision, as in the reference
  *    (vec3.h:7). The device computes in fp32 (RT_PREC_F32, the production
  *    path) or fp64 (RT_PREC_F64, the parity path).
@@ -39,7 +45,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 typedef enum rt_status {
   RT_OK = 0,
@@ -214,7 +220,9 @@ typedef struct rt_counters {
   uint64_t launches;   /* kernel launches */
   double last_render_ms; /* host time of the last rt_render_tiles call (enqueue time when asynchronous) */
   double step_ms; /* device time of the path-step kernels (when timing is enabled) */
-  double aux_ms;  /* reserved */
+  double aux_ms;  /* rt_multi_stats: device time of the gather + unpack; otherwise 0 */
+  uint64_t grid_lanes; /* lanes of the last persistent-kernel launch: the resident grid the occupancy
+                          query gave that kernel on this device */
 } rt_counters;
 
 /* What rt_scene_check / rt_scene_upload compiled a descriptor into. */
@@ -265,6 +273,40 @@ rt_status rt_set_timing(rt_context* ctx, int32_t enable);
 /* Counter-based RNG of the device path, evaluated on the host (for tests):
  * returns the 32-bit draw for (seed, pixel, sample, dim). */
 uint32_t rt_rng_u32(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t dim);
+
+/* ---- multi-GPU driver: the framebuffer tiled over the devices of one node ----
+ *
+ * Replaces camera::render's per-row std::for_each(par_unseq) (camera.h:154-172) when a
+ * scene is rendered on several GPUs. Tiles of tile_size x tile_size pixels (row-major
+ * over the image) are dealt round-robin: device k renders tiles k, k + n, k + 2n, ...
+ * packed in that order into a buffer padded to the largest device's pixel count; one
+ * ncclGather (RCCL over xGMI) brings the n buffers to devices[0], which unpacks them into
+ * the linear framebuffer (row 0 at the top, camera.h:170) and copies it to the host.
+ * Every pixel's samples are keyed by (seed, pixel, sample), so the image is bit-identical
+ * for any device count. A device list that repeats a device (tests on a one-GPU box)
+ * renders those ranks on the same device one after another and gathers with device copies
+ * instead of RCCL (rt_multi_uses_rccl says which). */
+typedef struct rt_multi rt_multi;
+
+rt_status rt_multi_create(const int32_t* devices, int32_t ndev, rt_multi** out);
+void rt_multi_destroy(rt_multi* m);
+/* Message of the last failing call on m (or the last create failure when m == NULL). */
+const char* rt_multi_last_error(const rt_multi* m);
+/* 1 when the gather runs through an RCCL communicator, 0 for the device-copy gather. */
+int32_t rt_multi_uses_rccl(const rt_multi* m);
+/* rt_scene_upload on every device. */
+rt_status rt_multi_scene_upload(rt_multi* m, const rt_scene_desc* desc);
+/* The whole image into out_rgb: host memory, W * H * 3 floats (RT_PREC_F32) or doubles (RT_PREC_F64),
+ * row-major, top row first. tile_size <= 0 selects 32. */
+rt_status rt_multi_render(rt_multi* m, const rt_camera_desc* cam, const rt_render_params* params,
+                          int32_t tile_size, void* out_rgb);
+/* Counters of rank `rank` (0 <= rank < ndev) since rt_multi_create; aux_ms of rank 0 holds the
+ * device time of the last gather + unpack. */
+rt_status rt_multi_stats(rt_multi* m, int32_t rank, rt_counters* out);
+/* Host-only tile plan: writes rank `rank`'s tiles (at most cap; tiles_out may be NULL) and returns
+ * how many it has, or -1 for invalid arguments. */
+int32_t rt_multi_plan(int32_t width, int32_t height, int32_t ndev, int32_t tile_size, int32_t rank,
+                      rt_tile* tiles_out, int32_t cap);
 
 #ifdef __cplusplus
 }

@@ -28,7 +28,7 @@ def test_every_declared_symbol_is_exported():
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(abi.SIGNATURES), set(names) ^ set(abi.SIGNATURES)
-    assert lib.rt_abi_version() == abi.ABI_VERSION == 4
+    assert lib.rt_abi_version() == abi.ABI_VERSION == 5
 
 
 def test_struct_layout_matches_c(tmp_path):
@@ -124,3 +124,14 @@ def test_big_scene_gets_a_bvh_within_the_stack():
     st, info, msg = abi.scene_check(s.desc(s.bvh(tris)))
     assert st == abi.RT_OK, msg
     assert info.triangles == 20000 and info.linear_ops == 0 and info.stack_need <= 32
+
+
+def test_multi_create_without_device_fails_cleanly():
+    import torch
+    if torch.cuda.device_count() > 0:
+        pytest.skip("a GPU is present")
+    lib = abi.load()
+    h = ctypes.c_void_p()
+    devs = (ctypes.c_int32 * 2)(0, 1)
+    assert lib.rt_multi_create(devs, 2, ctypes.byref(h)) == abi.RT_ERR_NO_DEVICE
+    assert not h.value and b"device" in lib.rt_multi_last_error(None)
