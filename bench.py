@@ -25,10 +25,14 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import rt_amd  # noqa: E402
-from rt_amd import abi, plugin  # noqa: E402
+from rt_amd import abi, buildinfo, plugin  # noqa: E402
 from rt_amd.tiling import pixel_index, plan  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD every 2 cycles at the
+# 2.4 GHz max clock (MI355X_MICROARCH.md, "Wave scheduling")
+SIMDS, CLOCK_GHZ, VALU_CYCLES = 1024, 2.4, 2
+VALU_PEAK_G = SIMDS * CLOCK_GHZ / VALU_CYCLES  # G wave-instructions/s
 # SURVEY.md §8(d) algorithmic bytes: per sample (generate + finalise) and per segment
 B_GEN, B_ACC, B_EXT, B_SHADE = 64, 36, 44, 152
 
@@ -55,37 +59,71 @@ def sponza_asset():
     return path, "synthetic Sponza stand-in (rt_amd.synth_gltf, 262,267 triangles; Sponza.bin is not shipped)"
 
 
-def cpu_baseline(scene_name, width, aspect, spp, depth, seed, threads):
-    """The oracle (fp64 restatement of the reference loop) on host cores, over a row sample."""
+def cpu_threads():
+    """Threads for the CPU baseline: every CPU this process may use, capped by the box's CPU share
+    (cgroup quota, or OMP_NUM_THREADS, which the GPU box sets to its share)."""
+    info = buildinfo.host_cpu()
+    n = info["affinity"]
+    if info["cgroup_quota_cpus"]:
+        n = min(n, max(1, int(info["cgroup_quota_cpus"])))
+    if info["omp_num_threads"]:
+        try:
+            n = min(n, max(1, int(info["omp_num_threads"])))
+        except ValueError:
+            pass
+    return n, info
+
+
+def cpu_baseline(scene_name, width, aspect, spp, depth, seed, threads, target_msamples):
+    """The oracle (fp64 restatement of the reference loop, counter RNG) on host cores, over a row sample.
+    Returns (the bench line's cpu_baseline object, the rows rendered, their fp64 pixels)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
     cs = plugin.ConfigScene(scene_name, width, aspect)
     cam = cs.cam
     osc = oracle.from_desc(cs.desc)
-    # about 80 Msamples (a few seconds on 16 cores): evenly spaced full rows at the full spp and depth
-    nrows = max(1, min(cam.image_height, int(80e6 // (cam.image_width * spp))))
+    # evenly spaced full rows at the full spp and depth, about target_msamples of work
+    nrows = max(1, min(cam.image_height, int(target_msamples * 1e6 // (cam.image_width * spp))))
     step = cam.image_height // nrows
     rows = list(range(0, cam.image_height, step))[:nrows]
     tiles = [(0, y, cam.image_width, 1) for y in rows]
     t0 = time.perf_counter()
-    oracle.render(osc, cam, spp, depth, seed=seed, threads=threads, tiles=tiles)
+    img, _ = oracle.render(osc, cam, spp, depth, seed=seed, threads=threads, tiles=tiles)
     dt = time.perf_counter() - t0
     n = len(rows) * cam.image_width * spp
-    return {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"oracle (fp64 C++ restatement, counter RNG) on {len(rows)} rows (every {step}th) x "
-                      f"{cam.image_width} px x {spp} spp, depth {depth}: {n / 1e6:.1f} Msamples in {dt:.1f} s"}
+    n_threads, info = threads, buildinfo.host_cpu()
+    line = {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": n_threads, "kind": "port",
+            "per_core": round(n / dt / 1e6 / n_threads, 4),
+            "host": info,
+            "sample": f"oracle (fp64 C++ restatement of camera.h:135-241, counter RNG, std::thread pool of "
+                      f"{n_threads}) on {len(rows)} rows (every {step}th) x {cam.image_width} px x {spp} spp, "
+                      f"depth {depth}: {n / 1e6:.1f} Msamples in {dt:.1f} s"}
+    return line, rows, img.reshape(len(rows), cam.image_width, 3)
 
 
-def measured_traffic(workload, kernel):
-    """HBM bytes per launch of the dominant kernel from the committed PMC summary of this exact workload and
-    kernel family (profiles/<tag>_traffic.json, written by scripts/pmc_summary.py; the last in name order
-    wins), or None."""
+def parity_rows(fb, W, rows, ref_rows):
+    """Per-channel RMSE of the GPU framebuffer rows against the oracle's rows (same seed, same sample
+    streams): SURVEY.md §8(c) link 3, at the full bench config."""
+    got = fb.reshape(-1, W, 3)[rows].double().cpu().numpy()
+    d = got - ref_rows
+    rmse = np.sqrt((d ** 2).reshape(-1, 3).mean(0))
+    return {"rmse": [float(f"{x:.3g}") for x in rmse], "max_abs": float(f"{np.abs(d).max():.3g}"),
+            "rows": len(rows), "pixels": int(d.shape[0] * d.shape[1]), "tolerance": 1e-4,
+            "pass": bool((rmse < 1e-4).all() and np.isfinite(got).all()),
+            "against": "oracle fp64, same seed and counter-RNG streams"}
+
+
+def measured_pmc(workload):
+    """Per-launch PMC figures of the dominant kernel for this exact workload and build (profiles/*_pmc.json,
+    written by scripts/pmc_summary.py from separate rocprofv3 --pmc passes; the last in name order wins),
+    or None when no pass was collected on this build."""
     found = None
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json"))):
+    sha = buildinfo.src_sha()
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json"))):
         with open(f) as fh:
             d = json.load(fh)
-        if d.get("workload") == workload and d.get("kernel") == kernel:
-            found = (os.path.basename(f), d["bytes_per_launch"])
+        if d.get("workload") == workload and d.get("src_sha") == sha:
+            found = (os.path.basename(f), d)
     return found
 
 
@@ -112,7 +150,13 @@ def main():
     ap.add_argument("--kernel-timing", default="on", choices=["on", "off"],
                     help="HIP events around every extend/shade launch of the timed steps (roofline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: the CPUs this process may use, capped by the "
+                                                                   "box's share (cgroup quota / OMP_NUM_THREADS)")
+    ap.add_argument("--cpu-msamples", type=float, default=240.0,
+                    help="size of the CPU-baseline row sample (Msamples of oracle work)")
+    ap.add_argument("--f64-steps", type=int, default=3,
+                    help="after the headline run, time this many frames of the fp64 path (the reference's "
+                         "precision, vec3.h:7) on the same config; 0 = skip")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -132,87 +176,123 @@ def main():
     cam = cs.cam
     W, H = cam.image_width, cam.image_height
     prec = abi.RT_PREC_F64 if args.precision == "f64" else abi.RT_PREC_F32
-    tdtype = torch.float64 if prec == abi.RT_PREC_F64 else torch.float32
 
     ctx = rt_amd.Context(local)
     ctx.upload(cs.desc)
     all_tiles, counts, maxpix = plan(W, H, world)
     my_tiles = all_tiles[rank]
-    out = torch.zeros((maxpix, 3), dtype=tdtype, device=dev)
-    params = ctx.params(spp, depth, args.seed, prec, samples_per_item=args.chunk, pool_slots=args.pool,
-                        segments_per_launch=args.segments_per_launch,
-                        traversal=abi.RT_TRAV_ORDERED if args.traversal == "ordered" else abi.RT_TRAV_AUTO)
-    fb = gathered = scatter_idx = None
+    scatter_idx = None
     if rank == 0:
-        fb = torch.zeros((H * W, 3), dtype=tdtype, device=dev)
-        gathered = [torch.zeros_like(out) for _ in range(world)]
         scatter_idx = [torch.from_numpy(pixel_index(all_tiles[r], W)).to(dev) for r in range(world)]
 
-    def step():
-        stream = torch.cuda.current_stream(dev).cuda_stream
-        ctx.render_tiles(cam, params, my_tiles, out.data_ptr(), 1, stream)
-        if world > 1:
-            dist.gather(out, gathered if rank == 0 else None, dst=0)
-            parts = gathered
-        else:
-            parts = [out]
+    def run(precision, steps, warmup, timing):
+        """warmup + `steps` timed frames; returns (elapsed s (max over ranks), stats, rank 0's framebuffer)."""
+        tdtype = torch.float64 if precision == abi.RT_PREC_F64 else torch.float32
+        out = torch.zeros((maxpix, 3), dtype=tdtype, device=dev)
+        params = ctx.params(spp, depth, args.seed, precision, samples_per_item=args.chunk, pool_slots=args.pool,
+                            segments_per_launch=args.segments_per_launch,
+                            traversal=abi.RT_TRAV_ORDERED if args.traversal == "ordered" else abi.RT_TRAV_AUTO)
+        fb = gathered = None
         if rank == 0:
-            for r in range(world):
-                fb[scatter_idx[r]] = parts[r][: counts[r]]
+            fb = torch.zeros((H * W, 3), dtype=tdtype, device=dev)
+            gathered = [torch.zeros_like(out) for _ in range(world)]
 
-    for _ in range(args.warmup):
-        step()
-    ctx.set_timing(args.kernel_timing == "on")
-    ctx.reset_counters()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()  # stream-ordered: the host enqueues the next frame while the GPU renders this one
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    st = ctx.stats()  # totals over the timed steps (kernel time from HIP events on the render stream)
+        def step():
+            # torch's current stream (the default = the HIP null stream): the gather and the scatter
+            # below are queued behind the render on the same stream
+            stream = torch.cuda.current_stream(dev).cuda_stream
+            ctx.render_tiles(cam, params, my_tiles, out.data_ptr(), 1, stream)
+            if world > 1:
+                dist.gather(out, gathered if rank == 0 else None, dst=0)
+                parts = gathered
+            else:
+                parts = [out]
+            if rank == 0:
+                for r in range(world):
+                    fb[scatter_idx[r]] = parts[r][: counts[r]]
+
+        for _ in range(warmup):
+            step()
+        ctx.set_timing(timing)
+        ctx.reset_counters()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()  # stream-ordered: the host enqueues the next frame while the GPU renders this one
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        st = ctx.stats()  # totals over the timed steps (kernel time from HIP events on the render stream)
+        ctx.set_timing(False)
+        if world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        return elapsed, st, fb
+
+    elapsed, st, fb = run(prec, args.steps, args.warmup, args.kernel_timing == "on")
     segs, step_ms, iters = st.segments, st.step_ms, st.iterations
+    segs_total = float(segs)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
         s = torch.tensor([segs], dtype=torch.float64, device=dev)
         dist.all_reduce(s, op=dist.ReduceOp.SUM)
         segs_total = float(s.item())
-    else:
-        segs_total = float(segs)
-
     total_samples = W * H * spp * args.steps
     value = total_samples / elapsed / 1e6
+    f64_line = None
+    if args.f64_steps > 0 and prec == abi.RT_PREC_F32:
+        e64, st64, _ = run(abi.RT_PREC_F64, args.f64_steps, 1, False)
+        f64_line = {"value": round(W * H * spp * args.f64_steps / e64 / 1e6, 2), "unit": "Msamples/s",
+                    "steps": args.f64_steps, "ms_per_step": round(e64 / args.f64_steps * 1e3, 3),
+                    "dtype": "fp64", "note": "the same frames on the fp64 path (the reference's precision, "
+                                             "vec3.h:7), timed the same way after the headline run"}
+
     if rank == 0:
         my_samples = counts[0] * spp * args.steps
         seg_per_sample = segs / max(1, my_samples)
+        key = workload_key(scene_name, W, H, spp, depth, args)
         # dominant kernel of rank 0 (k_persist: the persistent extend+shade loop, one launch per frame;
-        # k_step with --segments-per-launch K: the fused wavefront step): algorithmic bytes of
-        # SURVEY.md §8(d) per launch / average launch duration from HIP events on the render stream
+        # k_step with --segments-per-launch K: the fused wavefront step), average launch duration from HIP
+        # events on the render stream. It is VALU-issue bound: path state stays in registers, so HBM
+        # moves ~0.1 % of the classic wavefront's bytes. achieved = VALU wave-instructions per launch
+        # (rocprofv3 SQ_INSTS_VALU of this build and workload, profiles/*_pmc.json) / live launch time.
         roof = None
         if args.kernel_timing == "on" and iters > 0:
             alg_bytes = (B_GEN + B_ACC) * my_samples + (B_EXT + B_SHADE) * segs
             avg_s = step_ms / 1e3 / iters
-            achieved = alg_bytes / (step_ms / 1e3) / 1e9
             kern = "k_step" if args.segments_per_launch > 0 else "k_persist"
-            mt = measured_traffic(workload_key(scene_name, W, H, spp, depth, args), kern)
-            roof = {"bound": "hbm", "kernel": kern, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": int(mt[1]) if mt else None,
+            mp = measured_pmc(key)
+            roof = {"bound": "valu", "kernel": kern, "unit": "G VALU wave-instr/s", "peak": VALU_PEAK_G,
+                    "achieved": None, "frac": None, "traffic": None,
                     "avg_launch_us": round(avg_s * 1e6, 2), "launches": iters,
-                    "alg_bytes_per_launch": int(alg_bytes / iters),
-                    "kernel_share_of_wall": round(step_ms / 1e3 / elapsed, 4)}
-            if mt:
-                roof["traffic_source"] = "profiles/" + mt[0]
-                roof["traffic_over_alg"] = round(mt[1] / (alg_bytes / iters), 4)
-        cpu = None
+                    "kernel_share_of_wall": round(step_ms / 1e3 / elapsed, 4),
+                    "peak_basis": "1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction",
+                    "wavefront_equiv": {"alg_bytes_per_launch": int(alg_bytes / iters),
+                                        "GBps": round(alg_bytes / (step_ms / 1e3) / 1e9, 1),
+                                        "note": "SURVEY §8(d) bytes a classic SoA wavefront would move for "
+                                                "this work; not HBM traffic"}}
+            if mp:
+                d = mp[1]
+                achieved = d["valu_per_launch"] / avg_s / 1e9
+                roof.update({"achieved": round(achieved, 2), "frac": round(achieved / VALU_PEAK_G, 4),
+                             "valu_per_launch": d["valu_per_launch"], "pmc_source": "profiles/" + mp[0],
+                             "frac_at_measured_clock": d.get("valu_issue_frac_measured_clock"),
+                             "lane_valu_per_segment": round(d["valu_per_launch"] * 64 / (segs / iters), 1)})
+                if d.get("hbm_bytes_per_launch") is not None:
+                    tb = d["hbm_bytes_per_launch"]
+                    roof["traffic"] = int(tb)
+                    roof["hbm"] = {"achieved_GBps": round(tb / avg_s / 1e9, 2), "peak_GBps": HBM_PEAK_GBS,
+                                   "frac": round(tb / avg_s / 1e9 / HBM_PEAK_GBS, 5)}
+                assert roof["frac"] <= 1.0, roof
+        cpu = parity = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(scene_name, width, aspect, spp, depth, args.seed, args.cpu_threads)
+            threads = args.cpu_threads or cpu_threads()[0]
+            cpu, rows, ref_rows = cpu_baseline(scene_name, width, aspect, spp, depth, args.seed, threads,
+                                               args.cpu_msamples)
+            parity = parity_rows(fb, W, rows, ref_rows)
         line = {
             "metric": "Msamples/sec (pixels*spp) Cornell Box 800x800@1024spp; 1/2/4/8-GPU scaling"
             if args.config == "c2" else f"Msamples/sec (pixels*spp) {scene_name} {W}x{H}@{spp}spp",
@@ -221,13 +301,15 @@ def main():
             "scaling": "strong", "vs_baseline": None, "dtype": "fp32" if prec == abi.RT_PREC_F32 else "fp64",
             "data": asset or "synthetic (the reference's scene, procedurally built; no assets)",
             "config": {"workload": f"{scene_name} {W}x{H} {spp}spp depth {depth}, light sampling on",
-                       "key": workload_key(scene_name, W, H, spp, depth, args),
+                       "key": key, "src_sha": buildinfo.src_sha(),
                        "image": [W, H], "spp": spp, "max_depth": depth, "tiles": "32x32 round-robin over ranks",
                        "parallelism": f"tiles{world}", "segments_per_sample": round(seg_per_sample, 4),
                        "segments_total": segs_total / args.steps, "kernel_timing": args.kernel_timing,
-                       "rounds_per_frame": iters // max(1, args.steps)},
+                       "rounds_per_frame": iters // max(1, args.steps), "grid_lanes": st.grid_lanes},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "parity": parity,
+            "f64": f64_line,
         }
         if cpu:
             line["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)

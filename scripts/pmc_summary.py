@@ -1,12 +1,14 @@
 #!/usr/bin/env python3
 """Summarise the rocprofv3 passes of scripts/prof_pmc.sh into profiles/.
 
-  python scripts/pmc_summary.py <prof dir> <tag> <workload>
+  python scripts/pmc_summary.py <prof dir> <tag> <workload> [<output dir>]
 
 Writes
   profiles/<tag>_kernel_stats.csv   the --kernel-trace --stats summary (copied as rocprofv3 wrote it)
   profiles/<tag>_pmc_summary.csv    per kernel and counter: dispatches, mean and total over the run
-  profiles/<tag>_traffic.json       HBM bytes per launch of the dominant kernel, read by bench.py for roofline.traffic
+  profiles/<tag>_pmc.json           per-launch figures of the dominant kernel, keyed by workload and
+                                    build (rt_amd.buildinfo.src_sha), read by bench.py for its roofline:
+                                    SQ_INSTS_VALU (VALU-issue roofline) and HBM bytes (roofline.traffic)
 
 HBM bytes follow MI355X_MICROARCH.md (HBM [CDNA4]): FETCH_SIZE and WRITE_SIZE are in KiB,
 and on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced read, so
@@ -34,7 +36,10 @@ def short(name):
 
 def main():
     prof, tag, workload = sys.argv[1], sys.argv[2], sys.argv[3]
-    out = os.path.join(REPO, "profiles")
+    # summaries land in profiles/ (here), or in the given directory (on the GPU box: under gpurun_out/,
+    # which gpurun copies back; then they are copied into profiles/ and committed)
+    out = sys.argv[4] if len(sys.argv) > 4 else os.path.join(REPO, "profiles")
+    os.makedirs(out, exist_ok=True)
     stats = glob.glob(os.path.join(prof, "trace", "*kernel_stats.csv"))
     if stats:
         shutil.copy(stats[0], os.path.join(out, f"{tag}_kernel_stats.csv"))
@@ -53,7 +58,7 @@ def main():
         w.writerows(rows)
     # the dominant kernel: all k_persist (default schedule) or k_step instantiations of the run
     fam = "k_persist" if any(k.startswith("k_persist") for k in acc) else "k_step"
-    fetch, write = [], []
+    fetch, write, traffic = [], [], None
     for k, counters in acc.items():
         if k.startswith(fam):
             fetch += counters.get("FETCH_SIZE", [])
@@ -65,9 +70,29 @@ def main():
                    "bytes_per_launch": (2.0 * f_mean + w_mean) * 1024.0,
                    "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (KiB; gfx950 FETCH_SIZE counts half, "
                               "MI355X_MICROARCH.md HBM [CDNA4])", "source": f"{tag}_pmc_summary.csv"}
-        with open(os.path.join(out, f"{tag}_traffic.json"), "w") as fh:
-            json.dump(traffic, fh, indent=1)
         print(json.dumps(traffic))
+    # everything bench.py's roofline needs, per launch of the dominant kernel family
+    def fam_mean(c):
+        v = [x for k, cs in acc.items() if k.startswith(fam) for x in cs.get(c, [])]
+        return (sum(v) / len(v), len(v)) if v else (None, 0)
+    valu, nv = fam_mean("SQ_INSTS_VALU")
+    gui, _ = fam_mean("GRBM_GUI_ACTIVE")
+    if valu is not None:
+        sys.path.insert(0, os.path.join(REPO, "cpu-ray-tracing-implementation_amd", "python"))
+        from rt_amd import buildinfo
+        d = {"workload": workload, "src_sha": buildinfo.src_sha(), "kernel": fam, "launches": nv,
+             "valu_per_launch": valu,
+             "valu_issue_frac_measured_clock": round(valu * 2 / (1024 * gui / 8), 4) if gui else None,
+             "grbm_gui_active_per_launch": gui,
+             "hbm_bytes_per_launch": traffic["bytes_per_launch"] if fetch and write else None,
+             "counters": {c: fam_mean(c)[0] for c in sorted({c for k, cs in acc.items() if k.startswith(fam)
+                                                             for c in cs})},
+             "formulas": {"valu_issue_frac_measured_clock": "SQ_INSTS_VALU * 2 / (1024 SIMDs * GRBM_GUI_ACTIVE / 8 "
+                                                            "XCDs)", "hbm_bytes": "(2*FETCH_SIZE + WRITE_SIZE) * 1024"},
+             "source": f"{tag}_pmc_summary.csv"}
+        with open(os.path.join(out, f"{tag}_pmc.json"), "w") as fh:
+            json.dump(d, fh, indent=1)
+        print(json.dumps(d))
 
 
 if __name__ == "__main__":

@@ -7,10 +7,10 @@ set -e
 out=$1; tag=$2; shift 2
 export TMPDIR=/tmp
 mkdir -p $out
-B="bench.py --steps 1 --warmup 1 --no-cpu-baseline --kernel-timing off $*"
+B="bench.py --steps 1 --warmup 1 --no-cpu-baseline --f64-steps 0 --kernel-timing off $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o run --output-format csv -- python3 $B > $out/trace.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU -d $out/pmc1 -o run --output-format csv -- python3 $B > $out/pmc1.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE -d $out/pmc2 -o run --output-format csv -- python3 $B > $out/pmc2.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS -d $out/pmc3 -o run --output-format csv -- python3 $B > $out/pmc3.log 2>&1
 key=$(python3 -c "import json; print([json.loads(l) for l in open('$out/trace.log') if l.startswith('{\"metric')][-1]['config']['key'])")
-python3 scripts/pmc_summary.py $out $tag "$key"
+python3 scripts/pmc_summary.py $out $tag "$key" $out/summary
