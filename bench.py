@@ -74,7 +74,7 @@ def cpu_threads():
     return n, info
 
 
-def cpu_baseline(scene_name, width, aspect, spp, depth, seed, threads, target_msamples):
+def cpu_baseline(scene_name, width, aspect, spp, depth, seed, threads, target_msamples, budget_s=20.0):
     """The oracle (fp64 restatement of the reference loop, counter RNG) on host cores, over a row sample.
     Returns (the bench line's cpu_baseline object, the rows rendered, their fp64 pixels)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -82,14 +82,26 @@ def cpu_baseline(scene_name, width, aspect, spp, depth, seed, threads, target_ms
     cs = plugin.ConfigScene(scene_name, width, aspect)
     cam = cs.cam
     osc = oracle.from_desc(cs.desc)
-    # evenly spaced full rows at the full spp and depth, about target_msamples of work
+    # evenly spaced full rows at the full spp and depth: about target_msamples of work, cut to what fits
+    # in budget_s on this host (one row is timed first); progress goes to stderr
     nrows = max(1, min(cam.image_height, int(target_msamples * 1e6 // (cam.image_width * spp))))
+    t0 = time.perf_counter()
+    first, _ = oracle.render(osc, cam, spp, depth, seed=seed, threads=threads, tiles=[(0, 0, cam.image_width, 1)])
+    t_row = time.perf_counter() - t0
+    nrows = max(1, min(nrows, int(budget_s / max(t_row, 1e-6))))
     step = cam.image_height // nrows
     rows = list(range(0, cam.image_height, step))[:nrows]
-    tiles = [(0, y, cam.image_width, 1) for y in rows]
-    t0 = time.perf_counter()
-    img, _ = oracle.render(osc, cam, spp, depth, seed=seed, threads=threads, tiles=tiles)
+    print(f"cpu_baseline: one row {t_row:.2f} s, rendering {len(rows)} rows", file=sys.stderr, flush=True)
+    parts = [first.reshape(1, cam.image_width, 3)]
+    for i in range(1, len(rows), 16):
+        batch = rows[i:i + 16]
+        img, _ = oracle.render(osc, cam, spp, depth, seed=seed, threads=threads,
+                               tiles=[(0, y, cam.image_width, 1) for y in batch])
+        parts.append(img.reshape(len(batch), cam.image_width, 3))
+        print(f"cpu_baseline: {i + len(batch)}/{len(rows)} rows, {time.perf_counter() - t0:.1f} s", file=sys.stderr,
+              flush=True)
     dt = time.perf_counter() - t0
+    img = np.concatenate(parts)
     n = len(rows) * cam.image_width * spp
     n_threads, info = threads, buildinfo.host_cpu()
     line = {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": n_threads, "kind": "port",
@@ -98,7 +110,7 @@ def cpu_baseline(scene_name, width, aspect, spp, depth, seed, threads, target_ms
             "sample": f"oracle (fp64 C++ restatement of camera.h:135-241, counter RNG, std::thread pool of "
                       f"{n_threads}) on {len(rows)} rows (every {step}th) x {cam.image_width} px x {spp} spp, "
                       f"depth {depth}: {n / 1e6:.1f} Msamples in {dt:.1f} s"}
-    return line, rows, img.reshape(len(rows), cam.image_width, 3)
+    return line, rows, img
 
 
 def parity_rows(fb, W, rows, ref_rows):
