@@ -17,9 +17,16 @@ RT_HDRS  := $(wildcard $(PKG)/rt/*.h) include/rt_hip.h
 
 all: $(BUILD)/librt_hip.so $(BUILD)/librt_scenes.so $(BUILD)/rt_main oracle
 
-$(BUILD)/librt_hip.so: $(LIB_SRCS) $(LIB_HDRS)
-	@mkdir -p $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(LIB_SRCS) -ldl
+# one object per source, so a host-only change does not recompile the kernels
+LIB_OBJS := $(BUILD)/obj/rt_kernels.o $(BUILD)/obj/rt_multi.o $(BUILD)/obj/scene_compile.o
+$(BUILD)/obj/%.o: $(PKG)/csrc/%.hip $(LIB_HDRS)
+	@mkdir -p $(BUILD)/obj
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+$(BUILD)/obj/%.o: $(PKG)/csrc/%.cpp $(LIB_HDRS)
+	@mkdir -p $(BUILD)/obj
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+$(BUILD)/librt_hip.so: $(LIB_OBJS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(LIB_OBJS) -ldl
 
 # development build with correctly rounded fp32 math (scripts/dev_divergence.py --lib)
 precise: $(BUILD)/librt_hip_precise.so

@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "rt_scene.h"
 #include "rt_sin.h"
 
@@ -229,6 +231,11 @@ struct DevScene {
   const double* texdata;  // procedural-texture tables (Texture::data)
   const uint8_t* images;  // picture-texture pixels (Texture::data)
   int32_t has_procedural; // any perlin / value / worley / voronoi texture: the EXT kernels
+  // wide BVH (fp32; rt_scene.h WNode): nodes, primitive words, root code, stack need, WK_* kinds
+  const WNode* wnodes;
+  const float4* wprims;
+  uint32_t n_wnodes, n_wprim_words, wroot, wide_stack, wide_kinds;
+  int32_t has_wide;
 };
 
 // World -> object through an instance chain (hittable.h:75-82, 125-135, 192-202, 259-270).
@@ -286,24 +293,27 @@ __device__ __forceinline__ bool box_hit(const R* lo, const R* hi, V<R> o, V<R> i
   return tn <= tf;
 }
 
-// quad::hit (quad.h:30-52) with the alpha/beta triple products precomputed.
+// quad::hit (quad.h:30-52) with the alpha/beta triple products precomputed (fields of Quad).
 template <class R>
-__device__ __forceinline__ bool quad_t(const Quad<R>& q, V<R> o, V<R> d, R tmin, R tmax, R& t) {
-  V<R> n = ld3(q.n);
-  R th = fdiv(q.D - dot(n, o), dot(n, d));
+__device__ __forceinline__ bool quad_test(V<R> n, R D, V<R> q, V<R> qa, V<R> qb, V<R> o, V<R> d, R tmin, R tmax,
+                                          R& t) {
+  R th = fdiv(D - dot(n, o), dot(n, d));
   if (!(tmin <= th && th <= tmax)) return false;  // interval::is_contains, NaN fails
-  V<R> p = (o + th * d) - ld3(q.q);
-  R a = dot(p, ld3(q.a)), b = dot(p, ld3(q.b));
+  V<R> p = (o + th * d) - q;
+  R a = dot(p, qa), b = dot(p, qb);
   if (!(R(0) <= a && a <= R(1) && R(0) <= b && b <= R(1))) return false;  // quad.h:58-64
   t = th;
   return true;
 }
+template <class R>
+__device__ __forceinline__ bool quad_t(const Quad<R>& q, V<R> o, V<R> d, R tmin, R tmax, R& t) {
+  return quad_test(ld3(q.n), q.D, ld3(q.q), ld3(q.a), ld3(q.b), o, d, tmin, tmax, t);
+}
 
 // triangle::hit / moller_trumbore (triangle.h:8-40).
 template <class R>
-__device__ __forceinline__ bool tri_t(const Tri<R>& tr, V<R> o, V<R> d, R tmin, R tmax, R& t) {
-  V<R> e1 = ld3(tr.e1), e2 = ld3(tr.e2);
-  V<R> s = o - ld3(tr.p0);
+__device__ __forceinline__ bool tri_test(V<R> p0, V<R> e1, V<R> e2, V<R> o, V<R> d, R tmin, R tmax, R& t) {
+  V<R> s = o - p0;
   V<R> s1 = cross(d, e2), s2 = cross(s, e1);
   R inv = fdiv(R(1), dot(s1, e1));
   R th = dot(s2, e2) * inv, b0 = dot(s1, s) * inv, b1 = dot(s2, d) * inv;
@@ -318,6 +328,10 @@ __device__ __forceinline__ bool tri_t(const Tri<R>& tr, V<R> o, V<R> d, R tmin, 
   if (th != th) return false;  // 0/0 determinant: the reference's comparisons reject NaN too
   t = th;
   return true;
+}
+template <class R>
+__device__ __forceinline__ bool tri_t(const Tri<R>& tr, V<R> o, V<R> d, R tmin, R tmax, R& t) {
+  return tri_test(ld3(tr.p0), ld3(tr.e1), ld3(tr.e2), o, d, tmin, tmax, t);
 }
 
 // sphere::hit (sphere.h:40-74). `far_only` is used for the sphere the ray
@@ -684,6 +698,141 @@ __device__ void trace(const DevScene<R>& sc, const Node<R>* nodes, V<R> wo, V<R>
   atomicAdd(&g_trace_totals[1], (unsigned long long)tc[1]);
   atomicAdd(&g_trace_totals[2], (unsigned long long)tc[2]);
 #endif
+}
+
+// Wide BVH traversal (fp32, rt_scene.h WNode): world-level primitives only, so no instance
+// state and no volume draws. Each node tests its four child boxes at once (independent slab
+// tests, which hide one another's latency), sorts the hits near-to-far with a 5-comparator
+// network on (t bits | slot) keys, continues with the nearest in a register and pushes the
+// others to the per-lane LDS stack (far first). Leaves walk their primitive words in place.
+// Primitive tests are the same functions as the other traversals (bit-identical hits); the
+// closest hit differs from the binary BVH's only on exact-t ties.
+// LDS copy of a node: 144-byte stride (36 dwords), so the 16 lanes of a ds_read_b128 group that
+// read 16 consecutive nodes hit 16 distinct 4-bank windows (a 128-byte stride gives 2).
+constexpr uint32_t kWNodeLdsStride = 144;
+// The traversal of one ray is resumable: (cur, sp, tmax, e_best) and the LDS stack are its whole
+// state. It returns true once the ray is finished, or false -- the ray paused -- when `pause` of
+// the wave's lanes that entered are finished and waiting: the persistent kernel then shades those
+// together and the paused lanes carry on beside the new rays (trace_wide callers in rt_kernels.hip).
+// Without the pause a wave would traverse until its slowest ray is done, its finished lanes idle.
+struct WideRay {
+  uint32_t cur;   // node index or leaf code to visit next
+  int32_t sp;     // entries on the LDS stack
+  float tmax;     // closest hit so far
+  uint32_t e;     // its entry (kNoHit: none)
+};
+// An LDS-resident tree (LDSN) is small: its child codes are rewritten to 16 bits when it is copied
+// into LDS (node index < 2^15, or 0x8000 | (count - 1) << 12 | first word < 2^12), which halves the
+// per-lane stack (uint16 entries) -- the LDS a block needs, and with it the blocks a CU can hold.
+constexpr uint32_t kWLeaf16 = 0x8000u;
+__host__ __device__ __forceinline__ uint32_t wide_code16(uint32_t c) {
+  return (c & kWLeaf) ? (kWLeaf16 | (((c >> kWCountShift) & 7u) << 12) | (c & 0xFFFu)) : c;
+}
+template <bool LDSN>
+using WStackT = typename std::conditional<LDSN, uint16_t, uint32_t>::type;
+template <bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN, int BLOCK, int PAUSE>
+__device__ __forceinline__ bool trace_wide(const DevScene<float>& sc, const unsigned char* lds_nodes,
+                                           const float4* lds_prims, V<float> o, V<float> d, float time,
+                                           uint32_t excl_e, WStackT<LDSN>* stk, WideRay& ry) {
+  constexpr uint32_t kLeafBit = LDSN ? kWLeaf16 : kWLeaf;
+  const float tmin = 0.001f;
+  const V<float> inv = box_inv(d);
+  const float4* prims = LDSN ? lds_prims : sc.wprims;
+  uint32_t keep_going = 0;  // pause at or below this many traversing lanes
+  if constexpr (PAUSE < 64) {
+    const uint32_t entered = (uint32_t)__popcll(__ballot(1));
+    keep_going = entered > (uint32_t)PAUSE ? entered - (uint32_t)PAUSE : 0u;
+  }
+  uint32_t cur = ry.cur;
+  int sp = ry.sp;
+  float tmax = ry.tmax;
+  uint32_t e_best = ry.e;
+  auto slab = [&](float lx, float ly, float lz, float hx, float hy, float hz, uint32_t c) {
+    const float tx0 = (lx - o.x) * inv.x, tx1 = (hx - o.x) * inv.x;
+    const float ty0 = (ly - o.y) * inv.y, ty1 = (hy - o.y) * inv.y;
+    const float tz0 = (lz - o.z) * inv.z, tz1 = (hz - o.z) * inv.z;
+    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
+    const float tf =
+        fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax)) * Num<float>::box_slack();
+    // tn >= tmin > 0: the bit pattern orders like the value; the low 2 bits carry the slot
+    return tn <= tf ? ((__float_as_uint(tn) & ~3u) | c) : 0xFFFFFFFFu;
+  };
+  bool done = false;
+  for (;;) {
+    while (!(cur & kLeafBit)) {  // inner nodes until this lane holds a leaf (while-while)
+      const float4* nd = LDSN ? (const float4*)(lds_nodes + cur * kWNodeLdsStride) : (const float4*)(sc.wnodes + cur);
+      const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
+      uint32_t k0 = slab(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, 0u);
+      uint32_t k1 = slab(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, 1u);
+      uint32_t k2 = slab(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, 2u);
+      uint32_t k3 = slab(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, 3u);
+#define RT_CS(a, b)                 \
+  {                                 \
+    const uint32_t lo_ = min(a, b); \
+    b = max(a, b);                  \
+    a = lo_;                        \
+  }
+      RT_CS(k0, k1);
+      RT_CS(k2, k3);
+      RT_CS(k0, k2);
+      RT_CS(k1, k3);
+      RT_CS(k1, k2);
+#undef RT_CS
+      if (k0 == 0xFFFFFFFFu) {  // no child hit
+        if (sp == 0) {
+          done = true;
+          break;
+        }
+        cur = stk[(--sp) * BLOCK];
+        continue;
+      }
+      const uint32_t* ch = (const uint32_t*)(nd + 6);
+      if (k3 != 0xFFFFFFFFu) stk[(sp++) * BLOCK] = ch[k3 & 3u];
+      if (k2 != 0xFFFFFFFFu) stk[(sp++) * BLOCK] = ch[k2 & 3u];
+      if (k1 != 0xFFFFFFFFu) stk[(sp++) * BLOCK] = ch[k1 & 3u];
+      cur = ch[k0 & 3u];
+    }
+    if (done) break;
+    uint32_t w = LDSN ? (cur & 0xFFFu) : (cur & kWFirstMask);
+    for (uint32_t n = (LDSN ? ((cur >> 12) & 7u) : ((cur >> kWCountShift) & 63u)) + 1u; n > 0; n--) {
+      const float4 h = prims[w];
+      const uint32_t e = __float_as_uint(h.w);
+      const uint32_t ty = etype(e);
+      float th;
+      bool hit = false;
+      if (SPH && (!(TRI || QUAD) || ty == E_SPHERE)) {
+        const float4 b = prims[w + 1];
+        w += 2;
+        hit = sphere_test(mkv(h.x, h.y, h.z), mkv(b.x, b.y, b.z), b.w, MOV, o, d, time, tmin, tmax, e == excl_e, th);
+      } else if (TRI && (!QUAD || ty == E_TRI)) {
+        const float4 a = prims[w + 1], b = prims[w + 2];
+        w += 3;
+        hit = e != excl_e && tri_test(mkv(h.x, h.y, h.z), mkv(a.x, a.y, a.z), mkv(b.x, b.y, b.z), o, d, tmin, tmax, th);
+      } else if (QUAD) {
+        const float4 nD = prims[w + 1], qa = prims[w + 2], qb = prims[w + 3];
+        w += 4;
+        hit = e != excl_e && quad_test(mkv(nD.x, nD.y, nD.z), nD.w, mkv(h.x, h.y, h.z), mkv(qa.x, qa.y, qa.z),
+                                       mkv(qb.x, qb.y, qb.z), o, d, tmin, tmax, th);
+      }
+      if (hit) {
+        tmax = th;
+        e_best = e;
+      }
+    }
+    if (sp == 0) {
+      done = true;
+      break;
+    }
+    cur = stk[(--sp) * BLOCK];
+    if constexpr (PAUSE < 64) {
+      if ((uint32_t)__popcll(__ballot(1)) <= keep_going) break;  // enough of the wave waits to be shaded
+    }
+  }
+  ry.cur = cur;
+  ry.sp = sp;
+  ry.tmax = tmax;
+  ry.e = e_best;
+  return done;
 }
 
 // Linear program (small scenes, rt_scene.h): every lane walks the same ops, so

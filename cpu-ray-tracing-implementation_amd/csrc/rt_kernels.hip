@@ -29,6 +29,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <tuple>
 #include <mutex>
 #include <new>
 #include <stdexcept>
@@ -49,6 +50,9 @@ constexpr int kBlock = 256;
 #endif
 #ifndef RT_LINEAR_WAVES
 #define RT_LINEAR_WAVES 6
+#endif
+#ifndef RT_SPHERE_REFINE  // fp32 sphere hits: point and normal from an fp64 re-solve (shade)
+#define RT_SPHERE_REFINE 1
 #endif
 #ifndef RT_PERSIST_MODE  // 2: dynamic (per-XCD heads), 1: static striding (development A/B)
 #define RT_PERSIST_MODE 2
@@ -455,8 +459,33 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
                    vz = (double)oo.z + (double)t * dd.z - cz;
             double k = (double)sp.r / sqrt(vx * vx + vy * vy + vz * vz);
             po = mkv((float)(cx + vx * k), (float)(cy + vy * k), (float)(cz + vz * k));
+            outward = (po - ld3(sp.cn)) * fdiv(R(1), sp.r);
+          } else {
+#if RT_SPHERE_REFINE
+            // The hit re-solved in fp64 from the fp32 ray (the root nearest the fp32 t), and the
+            // point and normal (sphere.h:67-69) built from it: the fp32 root is ~1e-6 off along
+            // the ray for t ~ 10, which tilts a small sphere's normal by ~1e-5 -- enough for a
+            // chain of mirror / glass bounces to leave the fp64 path a few times per million
+            // segments. This costs one fp64 quadratic per sphere hit.
+            const double cx = (double)sp.c1[0] + (double)s.tm * sp.dc[0], cy = (double)sp.c1[1] + (double)s.tm * sp.dc[1],
+                         cz = (double)sp.c1[2] + (double)s.tm * sp.dc[2];
+            const double ox = oo.x, oy = oo.y, oz = oo.z, dx = dd.x, dy = dd.y, dz = dd.z;
+            const double fx = ox - cx, fy = oy - cy, fz = oz - cz, rr = sp.r;
+            const double a = dx * dx + dy * dy + dz * dz, bh = dx * fx + dy * fy + dz * fz;
+            const double disc = bh * bh - a * ((fx * fx + fy * fy + fz * fz) - rr * rr);
+            double td = t;
+            if (disc >= 0) {
+              const double ia = 1.0 / a, sq = sqrt(disc);
+              const double t0 = (-bh - sq) * ia, t1 = (-bh + sq) * ia;
+              td = fabs(t0 - (double)t) <= fabs(t1 - (double)t) ? t0 : t1;
+            }
+            const double px = ox + td * dx, py = oy + td * dy, pz = oz + td * dz, ir = 1.0 / rr;
+            po = mkv((float)px, (float)py, (float)pz);
+            outward = mkv((float)((px - sp.cn[0]) * ir), (float)((py - sp.cn[1]) * ir), (float)((pz - sp.cn[2]) * ir));
+#else
+            outward = (po - ld3(sp.cn)) * fdiv(R(1), sp.r);
+#endif
           }
-          outward = (po - ld3(sp.cn)) * fdiv(R(1), sp.r);
         }
         mat = sp.mat;
         if constexpr (CAMX) sphere_uv(outward, hu, hv);  // sphere.h:70
@@ -618,6 +647,7 @@ struct LinearTrav {
                                                           : 1;
   static constexpr int kLdsNodes = 0;
   static constexpr bool kFlat = false;
+  static constexpr bool kWide = false;
   __device__ __forceinline__ static void run(const DevScene<R>& sc, const Node<R>*, const Path<R>& s, Keys k,
                                              uint32_t*, R& t, uint32_t& e, int32_t& i, uint32_t&) {
     trace_linear<R, SPH, TRI, VOL>(sc, s.o, s.d, s.tm, s.xe, s.xi, k, (uint32_t)s.bounce, t, e, i);
@@ -632,6 +662,7 @@ struct FlatTrav {
   static constexpr int kWaves = RT_FLAT_WAVES;
   static constexpr int kLdsNodes = 0;
   static constexpr bool kFlat = true;
+  static constexpr bool kWide = false;
   __device__ __forceinline__ static void run(const DevScene<float>& sc, const Node<float>*, const Path<float>& s,
                                              Keys, uint32_t*, float& t, uint32_t& e, int32_t& i, uint32_t& nm) {
     trace_flat(sc, s.o, s.d, s.xe, s.xi, t, e, i, nm);
@@ -646,10 +677,63 @@ struct StackTrav {
   static constexpr int kLdsNodes = LDSN ? (int)kLdsNodeMax : 0;
   static constexpr int kWaves = sizeof(R) == 4 ? RT_STACK_WAVES : 1;  // fp32: occupancy over a small spill
   static constexpr bool kFlat = false;
+  static constexpr bool kWide = false;
   __device__ __forceinline__ static void run(const DevScene<R>& sc, const Node<R>* nodes, const Path<R>& s, Keys k,
                                              uint32_t* stk, R& t, uint32_t& e, int32_t& i, uint32_t&) {
     trace<R, STACK, kBlock>(sc, LDSN ? nodes : sc.nodes, s.o, s.d, s.tm, s.xe, s.xi, k, (uint32_t)s.bounce, stk,
                             t, e, i);
+  }
+};
+
+// The wide BVH (fp32, rt_device.h trace_wide). LDSN: the whole tree -- nodes and primitive
+// words -- is copied into the block's dynamic LDS at kernel start; the per-lane stack follows it
+// ([depth][lane], conflict-free). Otherwise nodes and primitives are read from global memory and
+// only the stack is in LDS. Dynamic LDS is sized from the compiled scene (wide_lds_bytes).
+#ifndef RT_WIDE_WAVES  // LDS-resident tree: 6 blocks of 26 KB per CU (C3: 4 waves 93.6 ms, 5: 86.2, 6: 83.0)
+#define RT_WIDE_WAVES 6
+#endif
+#ifndef RT_WIDE_WAVES_GLOBAL  // tree in HBM, 32-bit stack in LDS (C4 stand-in: 4 waves 519 ms, 5: 462)
+#define RT_WIDE_WAVES_GLOBAL 5
+#endif
+#ifndef RT_SHADE_BATCH  // < 64: a wave stops traversing to shade once this many of its lanes have finished
+#define RT_SHADE_BATCH 64  // (measured on C3: 16 / 32 / 48 are 1-2 % slower than never pausing)
+#endif
+template <bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN>
+struct WideTrav {
+  static constexpr int kStack = 0;
+  static constexpr int kLdsNodes = 0;
+  static constexpr int kWaves = LDSN ? RT_WIDE_WAVES : RT_WIDE_WAVES_GLOBAL;
+  static constexpr bool kFlat = false;
+  static constexpr bool kWide = true;
+  using StackT = WStackT<LDSN>;
+  // LDS layout: [nodes, kWNodeLdsStride each][primitive words][stack: entries x kBlock of StackT]
+  __host__ __device__ static uint32_t stack_offset(uint32_t n_wnodes, uint32_t n_words) {
+    return LDSN ? n_wnodes * kWNodeLdsStride + n_words * 16u : 0u;
+  }
+  __host__ __device__ static uint32_t root(const DevScene<float>& sc) { return LDSN ? wide_code16(sc.wroot) : sc.wroot; }
+  __device__ __forceinline__ static StackT* fill(const DevScene<float>& sc, uint4* lds) {
+    unsigned char* base = (unsigned char*)lds;
+    if constexpr (LDSN) {
+      const uint4* gn = (const uint4*)sc.wnodes;  // 8 words of 16 B per node, the last one padding
+      for (uint32_t j = threadIdx.x; j < sc.n_wnodes * 7u; j += kBlock) {
+        const uint32_t nd = j / 7u, f = j - nd * 7u;
+        uint4 v = gn[nd * 8u + f];
+        if (f == 6) v = make_uint4(wide_code16(v.x), wide_code16(v.y), wide_code16(v.z), wide_code16(v.w));
+        *(uint4*)(base + nd * kWNodeLdsStride + f * 16u) = v;
+      }
+      uint4* pw = (uint4*)(base + sc.n_wnodes * kWNodeLdsStride);
+      const uint4* gp = (const uint4*)sc.wprims;
+      for (uint32_t j = threadIdx.x; j < sc.n_wprim_words; j += kBlock) pw[j] = gp[j];
+      __syncthreads();
+    }
+    return (StackT*)(base + stack_offset(sc.n_wnodes, sc.n_wprim_words));
+  }
+  // Advance the ray of s (false: paused, see trace_wide)
+  __device__ __forceinline__ static bool steps(const DevScene<float>& sc, const Node<float>* lds, const Path<float>& s,
+                                               StackT* stk, WideRay& ry) {
+    const unsigned char* base = (const unsigned char*)lds;
+    return trace_wide<SPH, TRI, QUAD, MOV, LDSN, kBlock, RT_SHADE_BATCH>(
+        sc, base, (const float4*)(base + sc.n_wnodes * kWNodeLdsStride), s.o, s.d, s.tm, s.xe, stk, ry);
   }
 };
 
@@ -749,6 +833,14 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
     for (uint32_t j = threadIdx.x; j < p.sc.n_nodes; j += kBlock) lds_nodes[j] = p.sc.nodes[j];
     __syncthreads();
   }
+  uint32_t* stk_lane = stk.v + threadIdx.x;
+  const Node<R>* trav_nodes = lds_nodes;
+  [[maybe_unused]] void* wstk = nullptr;  // the wide traversal's lane stack (uint16 or uint32 entries)
+  if constexpr (Trav::kWide) {
+    extern __shared__ uint4 dyn_lds[];
+    wstk = Trav::fill(p.sc, dyn_lds) + threadIdx.x;
+    trav_nodes = (const Node<R>*)dyn_lds;
+  }
   uint32_t item0 = blockIdx.x * kBlock + threadIdx.x;
   if (p.persist == 2) {
     if ((threadIdx.x & 63) == 0) {
@@ -763,17 +855,36 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
     s.acc = mkv(R(0), R(0), R(0));
     begin_item(p, s, item0);
     begin_sample<R, CAMX>(p, s);
+    if constexpr (Trav::kWide) {
+      // resumable traversal: a ray paused with the wave's laggards carries on after the others shade
+      using StackT = typename Trav::StackT;
+      const uint32_t root = Trav::root(p.sc);
+      WideRay ry{root, 0, Num<float>::inf(), kNoHit};
 #pragma unroll 1
-    for (;;) {
-      R t;
-      uint32_t e, nm = 0;
-      int32_t inst;
-      Trav::run(p.sc, lds_nodes, s, Keys{s.ks}, stk.v + threadIdx.x, t, e, inst, nm);
-      if (++segs > p.seg_cap) {  // cannot happen: every segment advances a bounce-capped path
-        atomicOr(p.fault, 1u);
-        break;
+      for (;;) {
+        if (!Trav::steps(p.sc, trav_nodes, s, (StackT*)wstk, ry)) continue;
+        if (++segs > p.seg_cap) {  // cannot happen: every segment advances a bounce-capped path
+          atomicOr(p.fault, 1u);
+          break;
+        }
+        const float t = ry.tmax;
+        const uint32_t e = ry.e;
+        ry = WideRay{root, 0, Num<float>::inf(), kNoHit};
+        if (!shade<R, CAMX, false>(p, s, t, e, -1, 0)) break;
       }
-      if (!shade<R, CAMX, Trav::kFlat>(p, s, t, e, inst, nm)) break;
+    } else {
+#pragma unroll 1
+      for (;;) {
+        R t;
+        uint32_t e, nm = 0;
+        int32_t inst;
+        Trav::run(p.sc, trav_nodes, s, Keys{s.ks}, stk_lane, t, e, inst, nm);
+        if (++segs > p.seg_cap) {  // cannot happen: every segment advances a bounce-capped path
+          atomicOr(p.fault, 1u);
+          break;
+        }
+        if (!shade<R, CAMX, Trav::kFlat>(p, s, t, e, inst, nm)) break;
+      }
     }
   }
   uint32_t sg = (uint32_t)segs;
@@ -981,8 +1092,14 @@ struct rt_context {
   // inputs kept on the device while they do not change between calls
   std::vector<uint4> tiles_dev;  // the tile list k_pixmap last expanded into pixmap
   void* pixmap_for = nullptr;    // pixmap buffer that expansion went to
+  uint32_t pixmap_npix = 0;      // pixels it expanded: a tile entry {x0, y0, width, first} does not
+                                 // hold the height, so the last tile can change with the list equal
   CamDev cam_dev{};              // the camera view in camx
   bool cam_valid = false;
+  // the compiled scene is copied into scene32 / scene64 by the first render after rt_scene_upload,
+  // on that render's stream: a copy made on another stream is not guaranteed visible to the kernels
+  // of the render stream (their launch need not invalidate the L2 lines of the previous scene)
+  bool scene_dirty32 = false, scene_dirty64 = false;
 };
 
 namespace {
@@ -1099,6 +1216,14 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
   s.texdata = (const double*)at(h.off_texdata);
   s.images = (const uint8_t*)at(h.off_images);
   s.has_procedural = h.n_texdata > 0 || h.has_cell_noise;
+  s.has_wide = (int32_t)h.has_wide;
+  s.wnodes = (const WNode*)at(h.off_wnodes);
+  s.wprims = (const float4*)at(h.off_wprims);
+  s.n_wnodes = h.n_wnodes;
+  s.n_wprim_words = h.n_wprim_words;
+  s.wroot = h.wroot;
+  s.wide_stack = h.wide_stack;
+  s.wide_kinds = h.wide_kinds;
   return s;
 }
 
@@ -1106,18 +1231,18 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
 // device): every persistent kernel has its own register budget, so one kernel's grid must not
 // size another's. Guarded: contexts on different host threads launch concurrently.
 std::mutex g_occ_mu;
-std::map<std::pair<const void*, int>, uint32_t> g_occ;
+std::map<std::tuple<const void*, int, size_t>, uint32_t> g_occ;
 
-uint32_t resident_blocks(const void* kern, int dev) {
+uint32_t resident_blocks(const void* kern, int dev, size_t lds) {
   std::lock_guard<std::mutex> lk(g_occ_mu);
-  auto it = g_occ.find({kern, dev});
+  auto it = g_occ.find({kern, dev, lds});
   if (it != g_occ.end()) return it->second;
   int n = 0, b = 0;
   uint32_t r = 0;  // unknown: keep the host's grid
   if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, kBlock, 0) == hipSuccess && b > 0 && n > 0)
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, kBlock, lds) == hipSuccess && b > 0 && n > 0)
     r = (uint32_t)(b * n);
-  g_occ[{kern, dev}] = r;
+  g_occ[{kern, dev, lds}] = r;
   return r;
 }
 
@@ -1125,10 +1250,10 @@ uint32_t resident_blocks(const void* kern, int dev) {
 thread_local uint64_t t_grid_lanes = 0;
 
 template <class KernelT, class R>
-void launch_one(KernelT kern, Params<R> p, uint32_t grid, hipStream_t st) {
+void launch_one(KernelT kern, Params<R> p, uint32_t grid, hipStream_t st, size_t lds = 0) {
   if (p.persist == 2) {  // as many blocks as the chip holds resident; lanes pull items
     int dev = 0;
-    const uint32_t res = hipGetDevice(&dev) == hipSuccess ? resident_blocks((const void*)kern, dev) : 0;
+    const uint32_t res = hipGetDevice(&dev) == hipSuccess ? resident_blocks((const void*)kern, dev, lds) : 0;
     if (res > 0) grid = std::min<uint32_t>(grid, res);
     p.P = grid * kBlock;
     p.seg_cap = (uint64_t)p.n_items * p.chunk * (uint64_t)p.max_depth + 1;
@@ -1137,7 +1262,34 @@ void launch_one(KernelT kern, Params<R> p, uint32_t grid, hipStream_t st) {
     p.seg_cap = ((uint64_t)p.n_items + p.P - 1) / p.P * p.chunk * (uint64_t)p.max_depth + 1;
   }
   if (p.persist) t_grid_lanes = (uint64_t)grid * kBlock;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, st, p);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, st, p);
+}
+
+// Dynamic LDS of a wide-BVH launch: the whole tree when it fits the budget (LDSN), else the stack only.
+constexpr size_t kWideLdsBudget = 40u << 10;  // bytes per 256-lane block: 4 blocks per CU of 160 KiB
+inline size_t wide_lds_bytes(const DevScene<float>& sc, bool ldsn) {
+  const size_t stack = (size_t)sc.wide_stack * kBlock * (ldsn ? 2u : 4u);  // uint16 entries in an LDS tree
+  return (ldsn ? (size_t)sc.n_wnodes * kWNodeLdsStride + (size_t)sc.n_wprim_words * 16u : 0u) + stack;
+}
+template <bool SPH, bool TRI, bool QUAD, bool MOV>
+void launch_wide_k(const Params<float>& p, uint32_t grid, hipStream_t st) {
+  const size_t full = wide_lds_bytes(p.sc, true);
+  // LDS-resident trees use 16-bit child codes (wide_code16): node index < 2^15, first word < 2^12
+  if (full <= kWideLdsBudget && p.sc.n_wnodes < 0x8000u && p.sc.n_wprim_words <= 0x1000u)
+    launch_one(k_persist_occ<float, WideTrav<SPH, TRI, QUAD, MOV, true>, false>, p, grid, st, full);
+  else
+    launch_one(k_persist_occ<float, WideTrav<SPH, TRI, QUAD, MOV, false>, false>, p, grid, st,
+               wide_lds_bytes(p.sc, false));
+}
+// Kernel for the primitive kinds of the scene: spheres only (RTOW), triangles only (meshes), or all.
+inline void launch_wide(const Params<float>& p, uint32_t grid, hipStream_t st) {
+  const uint32_t k = p.sc.wide_kinds;
+  if (k == WK_SPHERE)
+    launch_wide_k<true, false, false, false>(p, grid, st);
+  else if (k == WK_TRI)
+    launch_wide_k<false, true, false, false>(p, grid, st);
+  else
+    launch_wide_k<true, true, true, true>(p, grid, st);
 }
 template <class R, class Trav>
 void launch_k(const Params<R>& p, uint32_t grid, hipStream_t st) {
@@ -1179,6 +1331,18 @@ void launch_step(const Params<R>& p, int stack, bool sph, bool tri, uint32_t gri
       launch_k<R, LinearTrav<R, true, false, false>>(p, grid, st);
     else
       launch_k<R, LinearTrav<R, true, true, true>>(p, grid, st);
+  } else if constexpr (sizeof(R) == 4) {
+    if (p.sc.has_wide && p.persist && p.cam_mode == RT_CAM_PERSPECTIVE && !p.sc.has_procedural) {
+      launch_wide(p, grid, st);  // the wide BVH (persistent schedule, base kernels)
+    } else if (p.sc.n_nodes <= kLdsNodeMax && stack <= 16) {
+      launch_k<R, StackTrav<R, 16, true>>(p, grid, st);
+    } else if (stack <= 8) {
+      launch_k<R, StackTrav<R, 8>>(p, grid, st);
+    } else if (stack <= 16) {
+      launch_k<R, StackTrav<R, 16>>(p, grid, st);
+    } else {
+      launch_k<R, StackTrav<R, kStackDepth>>(p, grid, st);
+    }
   } else if (sizeof(R) == 4 && p.sc.n_nodes <= kLdsNodeMax && stack <= 16) {
     launch_k<R, StackTrav<R, 16, true>>(p, grid, st);
   } else if (stack <= 8) {
@@ -1197,10 +1361,16 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
   const CompiledScene& cs = c->scene;
   const SceneHeader& hdr = f64 ? cs.hdr64 : cs.hdr;
   void* sbase = f64 ? c->scene64.ptr : c->scene32.ptr;
+  bool& dirty = f64 ? c->scene_dirty64 : c->scene_dirty32;
   auto t0 = std::chrono::steady_clock::now();
   // A device-output render still pending on another stream reads the context's shared buffers
   // (pixmap, tiles, camx, heads, partial): wait for it before this call writes any of them.
   if (c->pending && c->pend_stream != st) RT_HIP(c, hipStreamSynchronize(c->pend_stream));
+  if (dirty) {  // the scene uploaded since the last render of this precision, stream-ordered before its kernels
+    const std::vector<unsigned char>& blob = f64 ? cs.blob64 : cs.blob32;
+    RT_HIP(c, hipMemcpyAsync(sbase, blob.data(), blob.size(), hipMemcpyHostToDevice, st));
+    dirty = false;
+  }
 
   // pixel map: tiles packed in order, row-major inside each tile (expanded by k_pixmap)
   std::vector<uint4> tl;
@@ -1255,12 +1425,13 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     if ((s = ensure(c, c->pixmap, 4ull * npix)) != RT_OK) return s;
     if (c->pixmap.bytes != pixmap_bytes) c->tiles_dev.clear();  // reallocated: the old map is gone
     if ((s = ensure(c, c->blk, 4ull * (nblk_max + 2))) != RT_OK) return s;
-    const bool same_tiles = c->pixmap_for == c->pixmap.ptr && c->tiles_dev.size() == tl.size() &&
+    const bool same_tiles = c->pixmap_for == c->pixmap.ptr && c->pixmap_npix == npix && c->tiles_dev.size() == tl.size() &&
                             std::memcmp(c->tiles_dev.data(), tl.data(), sizeof(uint4) * tl.size()) == 0;
     if (!same_tiles) {  // the pixel map of an unchanged tile list is still in pixmap
       if ((s = ensure(c, c->tiles, sizeof(uint4) * tl.size())) != RT_OK) return s;
       c->tiles_dev = tl;  // the copy's source outlives this call
       c->pixmap_for = c->pixmap.ptr;
+      c->pixmap_npix = npix;
       RT_HIP(c, hipMemcpyAsync(c->tiles.ptr, c->tiles_dev.data(), sizeof(uint4) * tl.size(), hipMemcpyHostToDevice,
                                st));
       hipLaunchKernelGGL(k_pixmap, dim3((npix + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
@@ -1270,7 +1441,7 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     unsigned char* sp = (unsigned char*)c->state.ptr;
     Params<R> p{};
     p.sc = dev_scene<R>(hdr, sbase);
-    if (prm->traversal == RT_TRAV_ORDERED) p.sc.has_flat = 0;
+    if (prm->traversal == RT_TRAV_ORDERED) p.sc.has_flat = p.sc.has_wide = 0;
     p.O = (R4<R>*)sp;
     p.D = (R4<R>*)(sp + r4);
     p.T = (R4<R>*)(sp + 2 * r4);
@@ -1472,12 +1643,12 @@ rt_status rt_scene_upload(rt_context* c, const rt_scene_desc* desc) {
   std::string err;
   rt_status s = compile_scene(desc, &cs, &err);
   if (s != RT_OK) return set_err(c, s, err);
+  // renders still pending on any stream read the current scene buffers
+  if (c->pending) RT_HIP(c, hipStreamSynchronize(c->pend_stream));
   if ((s = ensure(c, c->scene32, cs.blob32.size())) != RT_OK) return s;
   if ((s = ensure(c, c->scene64, cs.blob64.size())) != RT_OK) return s;
-  RT_HIP(c, hipMemcpyAsync(c->scene32.ptr, cs.blob32.data(), cs.blob32.size(), hipMemcpyHostToDevice, c->stream));
-  RT_HIP(c, hipMemcpyAsync(c->scene64.ptr, cs.blob64.data(), cs.blob64.size(), hipMemcpyHostToDevice, c->stream));
-  RT_HIP(c, hipStreamSynchronize(c->stream));
-  c->scene = std::move(cs);
+  c->scene = std::move(cs);  // copied to the device by the next render, on its stream (render<R>)
+  c->scene_dirty32 = c->scene_dirty64 = true;
   c->has_scene = true;
   return RT_OK;
 }
@@ -1493,6 +1664,10 @@ rt_status rt_scene_check(const rt_scene_desc* desc, rt_scene_info* info, char* e
     info->quads = cs.desc_quads;
     info->flat_quads = cs.flat_quads;
     info->flat_boxes = cs.flat_boxes;
+    info->wide_nodes = cs.hdr.has_wide ? (int32_t)cs.hdr.n_wnodes : 0;
+    info->wide_stack = cs.hdr.has_wide ? (int32_t)cs.hdr.wide_stack : 0;
+    info->wide_kinds = cs.hdr.has_wide ? (int32_t)cs.hdr.wide_kinds : 0;
+    info->wide_prim_words = cs.hdr.has_wide ? (int32_t)cs.hdr.n_wprim_words : 0;
     info->spheres = (int32_t)h.n_spheres;
     info->triangles = (int32_t)h.n_tris;
     info->instances = h.num_instances;

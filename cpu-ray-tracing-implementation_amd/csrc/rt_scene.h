@@ -175,6 +175,31 @@ struct alignas(16) Node {
   uint32_t child[2];
 };
 
+// The *wide BVH* (fp32 kernels): a 4-wide tree over world-level primitives, for scenes whose
+// world is primitives under lists / bvh_nodes only (no translate/rotate, no volume), e.g. the
+// RTOW spheres and glTF triangle meshes. One node is 128 B of structure-of-arrays child boxes,
+// read as six 16-byte loads; the primitives sit in leaf order in one stream of 16-byte words
+// (no reference indirection), in LDS when the whole tree fits:
+//   sphere   [c1.xyz, entry] [dc.xyz, r]
+//   triangle [p0.xyz, entry] [e1.xyz, -] [e2.xyz, -]
+//   quad     [q.xyz, entry] [n.xyz, D] [a.xyz, -] [b.xyz, -]       (fields of Quad)
+// `entry` (as bits) is the primitive's entry in quads/spheres/tris: shading and the
+// self-exclusion test use it exactly as for the other traversals.
+// child[c]: an inner node's index, or kWLeaf | (count - 1) << kWCountShift | first word;
+// unused slots have empty boxes (lo = hi = +inf on every axis: no ray direction hits them).
+struct alignas(16) WNode {
+  float lox[4], loy[4], loz[4];
+  float hix[4], hiy[4], hiz[4];
+  uint32_t child[4];
+  uint32_t pad[4];
+};
+constexpr uint32_t kWLeaf = 0x80000000u;
+constexpr uint32_t kWCountShift = 25;  // leaf: up to 64 primitives, first word < 2^25
+constexpr uint32_t kWFirstMask = (1u << kWCountShift) - 1u;
+constexpr int kWLeafMax = 4;
+// primitive kinds present (SceneHeader::wide_kinds)
+enum : uint32_t { WK_SPHERE = 1u, WK_TRI = 2u, WK_QUAD = 4u, WK_MOVING = 8u };
+
 enum : int32_t { M_LAMBERTIAN = 1, M_METAL = 2, M_DIELECTRIC = 3, M_ISOTROPIC = 4, M_DIFFUSE_LIGHT = 5, M_GLOSS = 6 };
 enum : int32_t { T_SOLID = 1, T_CHECKER = 2, T_PERLIN = 3, T_VALUE = 4, T_WORLEY = 5, T_VORONOI = 6, T_IMAGE = 7 };
 constexpr uint32_t kPerlinPoints = 256;  // noise.h:76 point_count
@@ -240,6 +265,13 @@ struct SceneHeader {
   uint32_t has_flat;            // 1: the flat program replaces the linear program in fp32
   uint64_t off_flat_quad, off_flat_box;
   uint32_t n_quads, n_spheres, n_tris, n_volumes, n_nodes, n_refs, n_mats, n_texs;
+  // wide BVH (fp32 blob only; has_wide = 0: none)
+  uint64_t off_wnodes, off_wprims;
+  uint32_t n_wnodes, n_wprim_words;
+  uint32_t wroot;        // root child code (a node index, or a leaf code for a tiny scene)
+  uint32_t wide_stack;   // traversal stack entries a lane can need
+  uint32_t wide_kinds;   // WK_* bits
+  uint32_t has_wide;
 };
 
 }  // namespace rtd

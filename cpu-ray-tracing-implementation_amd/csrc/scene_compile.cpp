@@ -20,6 +20,7 @@
 #include <unordered_map>
 #include <cmath>
 #include <cstring>
+#include <functional>
 #include <limits>
 #include <new>
 #include <stdexcept>
@@ -193,6 +194,7 @@ class Compiler {
   LinRec<double> lin_record(uint32_t op) const;
   bool flat_program(const std::vector<uint32_t>& lin, std::vector<FlatQuad>& quads, uint32_t nq[3],
                     std::vector<FlatBox>& boxes);
+  bool wide_bvh(const std::vector<Item>& prims, CompiledScene* out);
   std::vector<int> aligned_;  // per quad: 1 + perm for axis-aligned quads, 0 otherwise
   std::vector<double> qu_, qv_;  // per quad: u[U], v[V] (aligned quads)
   void light_from(int idx);
@@ -965,6 +967,220 @@ bool Compiler::flat_program(const std::vector<uint32_t>& lin, std::vector<FlatQu
   return true;
 }
 
+// The wide BVH of rt_scene.h (fp32 kernels) over world-level primitives: a binned SAH binary
+// tree, collapsed into 4-wide nodes by repeatedly opening the child of largest surface area.
+// Leaves hold their primitives' records in leaf order (no reference list). Closest hits do not
+// depend on the tree except on exact-t ties, as for the binary BVH.
+bool Compiler::wide_bvh(const std::vector<Item>& prims, CompiledScene* out) {
+  struct BN {
+    Box box;
+    int left = -1, right = -1;  // children (inner), or -1
+    size_t first = 0, count = 0;  // primitive range (leaf)
+  };
+  std::vector<BN> bn;
+  std::vector<size_t> order(prims.size());
+  for (size_t i = 0; i < order.size(); i++) order[i] = i;
+  std::vector<double> cen(prims.size() * 3);
+  for (size_t i = 0; i < prims.size(); i++)
+    for (int k = 0; k < 3; k++) cen[3 * i + k] = prims[i].box.center(k);
+  // binary build, iterative (meshes are deep); SAH with a node traversal cost of 1 primitive test
+  constexpr int kBins = 32;
+  bn.push_back(BN{});
+  bn[0].first = 0;
+  bn[0].count = prims.size();
+  std::vector<int> todo{0};
+  while (!todo.empty()) {
+    const int ni = todo.back();
+    todo.pop_back();
+    const size_t b = bn[(size_t)ni].first, n = bn[(size_t)ni].count, e = b + n;
+    Box bounds, cb;
+    for (size_t i = b; i < e; i++) {
+      bounds.grow(prims[order[i]].box);
+      cb.grow(&cen[3 * order[i]]);
+    }
+    bn[(size_t)ni].box = bounds;
+    if (n <= (size_t)kWLeafMax) continue;  // a leaf: one 4-wide node's worth of tests
+    int axis = 0;
+    for (int k = 1; k < 3; k++)
+      if (cb.hi[k] - cb.lo[k] > cb.hi[axis] - cb.lo[axis]) axis = k;
+    const double extent = cb.hi[axis] - cb.lo[axis];
+    size_t mid = b + n / 2;
+    bool split = false;
+    if (extent > 0) {
+      Box bin_box[kBins];
+      size_t bin_cnt[kBins] = {};
+      auto bin_of = [&](size_t p) {
+        int k = (int)((cen[3 * p + axis] - cb.lo[axis]) / extent * kBins);
+        return std::min(kBins - 1, std::max(0, k));
+      };
+      for (size_t i = b; i < e; i++) {
+        const int k = bin_of(order[i]);
+        bin_cnt[k]++;
+        bin_box[k].grow(prims[order[i]].box);
+      }
+      Box rb[kBins];
+      size_t rc[kBins] = {};
+      Box acc;
+      size_t cnt = 0;
+      for (int k = kBins - 1; k > 0; k--) {
+        acc.grow(bin_box[k]);
+        cnt += bin_cnt[k];
+        rb[k] = acc;
+        rc[k] = cnt;
+      }
+      double best = kInf;
+      int best_k = -1;
+      Box lb;
+      size_t lc = 0;
+      for (int s = 1; s < kBins; s++) {
+        lb.grow(bin_box[s - 1]);
+        lc += bin_cnt[s - 1];
+        if (!lc || !rc[s]) continue;
+        const double cost = lb.area() * (double)lc + rb[s].area() * (double)rc[s];
+        if (cost < best) {
+          best = cost;
+          best_k = s;
+        }
+      }
+      if (best_k > 0) {
+        auto it = std::partition(order.begin() + (long)b, order.begin() + (long)e,
+                                 [&](size_t p) { return bin_of(p) < best_k; });
+        mid = (size_t)(it - order.begin());
+        split = mid > b && mid < e;
+      }
+    }
+    if (!split) {
+      mid = b + n / 2;
+      std::nth_element(order.begin() + (long)b, order.begin() + (long)mid, order.begin() + (long)e,
+                       [&](size_t x, size_t y) { return cen[3 * x + axis] < cen[3 * y + axis]; });
+    }
+    const int l = (int)bn.size(), r = l + 1;
+    bn.push_back(BN{});
+    bn.push_back(BN{});
+    bn[(size_t)l].first = b;
+    bn[(size_t)l].count = mid - b;
+    bn[(size_t)r].first = mid;
+    bn[(size_t)r].count = e - mid;
+    bn[(size_t)ni].left = l;
+    bn[(size_t)ni].right = r;
+    todo.push_back(r);
+    todo.push_back(l);
+  }
+
+  // primitive records in leaf order
+  struct W4 {
+    float x, y, z, w;
+  };
+  std::vector<W4> words;
+  uint32_t kinds = 0;
+  auto bits = [](uint32_t u) {
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+  };
+  auto leaf_code = [&](const BN& nd, uint32_t& code) {
+    const size_t first = words.size();
+    if (nd.count == 0 || nd.count > 64 || first > kWFirstMask) return false;
+    for (size_t i = nd.first; i < nd.first + nd.count; i++) {
+      const uint32_t e = prims[order[i]].entry, ix = epay(e);
+      if (etype(e) == E_SPHERE) {
+        const Sphere<double>& s = spheres_[ix];
+        kinds |= WK_SPHERE | (s.moving ? WK_MOVING : 0u);
+        words.push_back({(float)s.c1[0], (float)s.c1[1], (float)s.c1[2], bits(e)});
+        words.push_back({(float)s.dc[0], (float)s.dc[1], (float)s.dc[2], (float)s.r});
+      } else if (etype(e) == E_TRI) {
+        const Tri<double>& t = tris_[ix];
+        kinds |= WK_TRI;
+        words.push_back({(float)t.p0[0], (float)t.p0[1], (float)t.p0[2], bits(e)});
+        words.push_back({(float)t.e1[0], (float)t.e1[1], (float)t.e1[2], 0.f});
+        words.push_back({(float)t.e2[0], (float)t.e2[1], (float)t.e2[2], 0.f});
+      } else if (etype(e) == E_QUAD) {
+        const Quad<double>& q = quads_[ix];
+        kinds |= WK_QUAD;
+        words.push_back({(float)q.q[0], (float)q.q[1], (float)q.q[2], bits(e)});
+        words.push_back({(float)q.n[0], (float)q.n[1], (float)q.n[2], (float)q.D});
+        words.push_back({(float)q.a[0], (float)q.a[1], (float)q.a[2], 0.f});
+        words.push_back({(float)q.b[0], (float)q.b[1], (float)q.b[2], 0.f});
+      } else {
+        return false;
+      }
+    }
+    code = kWLeaf | (uint32_t)(nd.count - 1) << kWCountShift | (uint32_t)first;
+    return true;
+  };
+
+  std::vector<WNode> wn;
+  // collapse: node of binary node `b` -> its index; stack need returned through `need`
+  std::function<bool(int, uint32_t&, int&)> emit = [&](int b, uint32_t& code, int& need) -> bool {
+    const BN& nd = bn[(size_t)b];
+    if (nd.left < 0) {
+      need = 0;
+      return leaf_code(nd, code);
+    }
+    std::vector<int> ch{nd.left, nd.right};
+    while (ch.size() < 4) {
+      int pick = -1;
+      double best = -1;
+      for (size_t k = 0; k < ch.size(); k++) {
+        const BN& c = bn[(size_t)ch[k]];
+        if (c.left >= 0 && c.box.area() > best) {
+          best = c.box.area();
+          pick = (int)k;
+        }
+      }
+      if (pick < 0) break;
+      const BN& c = bn[(size_t)ch[(size_t)pick]];
+      const int l = c.left, r = c.right;
+      ch[(size_t)pick] = l;
+      ch.insert(ch.begin() + pick + 1, r);
+    }
+    const size_t idx = wn.size();
+    if (idx >= kWLeaf) return false;
+    wn.emplace_back();
+    const float inf = std::numeric_limits<float>::infinity();
+    for (int c = 0; c < 4; c++) {
+      wn[idx].lox[c] = wn[idx].loy[c] = wn[idx].loz[c] = inf;
+      wn[idx].hix[c] = wn[idx].hiy[c] = wn[idx].hiz[c] = inf;
+      wn[idx].child[c] = kWLeaf;
+    }
+    int sub = 0;
+    for (size_t c = 0; c < ch.size(); c++) {
+      uint32_t cc;
+      int cn;
+      if (!emit(ch[c], cc, cn)) return false;
+      sub = std::max(sub, cn);
+      const Box& bx = bn[(size_t)ch[c]].box;
+      WNode& w = wn[idx];
+      w.lox[c] = down(bx.lo[0]);
+      w.loy[c] = down(bx.lo[1]);
+      w.loz[c] = down(bx.lo[2]);
+      w.hix[c] = up(bx.hi[0]);
+      w.hiy[c] = up(bx.hi[1]);
+      w.hiz[c] = up(bx.hi[2]);
+      w.child[c] = cc;
+    }
+    need = (int)ch.size() - 1 + sub;
+    code = (uint32_t)idx;
+    return true;
+  };
+  uint32_t root;
+  int need;
+  if (!emit(0, root, need)) return false;
+  if (need > kStackDepth) return false;
+  SceneHeader& h = out->hdr;
+  h.off_wnodes = append(out->blob32, wn);
+  h.off_wprims = append(out->blob32, words);
+  out->blob32.resize((out->blob32.size() + 255) & ~size_t(255));
+  h.bytes = out->blob32.size();
+  h.n_wnodes = (uint32_t)wn.size();
+  h.n_wprim_words = (uint32_t)words.size();
+  h.wroot = root;
+  h.wide_stack = (uint32_t)std::max(1, need);
+  h.wide_kinds = kinds;
+  h.has_wide = 1;
+  return true;
+}
+
 bool Compiler::run(CompiledScene* out, std::string* err) {
   if (!d_) {
     *err = "null scene descriptor";
@@ -1130,6 +1346,10 @@ bool Compiler::run(CompiledScene* out, std::string* err) {
     out->hdr.n_flat_box = (uint32_t)fb.size();
     out->hdr.has_flat = 1;
   }
+  // the wide BVH (fp32) when the world is a BVH over world-level primitives only
+  bool prims_only = etype(root.entry) == E_NODE;
+  for (const Item& it : top) prims_only = prims_only && etype(it.entry) <= E_TRI;
+  if (prims_only && !wide_bvh(top, out)) out->hdr.has_wide = 0;
   for (SceneHeader* h : {&out->hdr, &out->hdr64}) {
     h->has_cell_noise = cell_noise_ ? 1 : 0;
     h->root = root.entry;

@@ -26,7 +26,7 @@ RT_TEX_SOLID, RT_TEX_CHECKER, RT_TEX_PERLIN, RT_TEX_VALUE, RT_TEX_WORLEY, RT_TEX
 RT_CAM_PERSPECTIVE, RT_CAM_ORTHONORMAL, RT_CAM_FISHEYE, RT_CAM_LENS = range(4)
 RT_PREC_F32, RT_PREC_F64 = 0, 1
 RT_TRAV_AUTO, RT_TRAV_ORDERED = 0, 1
-ABI_VERSION = 5  # include/rt_hip.h RT_ABI_VERSION
+ABI_VERSION = 6  # include/rt_hip.h RT_ABI_VERSION
 
 
 class rt_object(ctypes.Structure):
@@ -80,7 +80,8 @@ class rt_counters(ctypes.Structure):
 class rt_scene_info(ctypes.Structure):
     _fields_ = [("quads", c_int32), ("spheres", c_int32), ("triangles", c_int32), ("instances", c_int32),
                 ("volumes", c_int32), ("bvh_nodes", c_int32), ("linear_ops", c_int32), ("stack_need", c_int32),
-                ("bytes_f32", c_uint64), ("bytes_f64", c_uint64), ("flat_quads", c_int32), ("flat_boxes", c_int32)]
+                ("bytes_f32", c_uint64), ("bytes_f64", c_uint64), ("flat_quads", c_int32), ("flat_boxes", c_int32),
+                ("wide_nodes", c_int32), ("wide_stack", c_int32), ("wide_kinds", c_int32), ("wide_prim_words", c_int32)]
 
 
 # every symbol include/rt_hip.h declares, with its ctypes signature

@@ -1,6 +1,7 @@
 // aabb.h -- axis-aligned box (reference: src/aabb.h:4-90). Kept for API
 // compatibility (get_bounding_box); the device builds its own BVH boxes.
 #pragma once
+#include "host_geometry.h"
 #include "interval.h"
 
 class aabb {
@@ -16,6 +17,7 @@ class aabb {
     return aabb(interval::enclose(a.x_, b.x_), interval::enclose(a.y_, b.y_), interval::enclose(a.z_, b.z_));
   }
   aabb offset(const vec3& o) const { return aabb(x_.offset(o.x()), y_.offset(o.y()), z_.offset(o.z())); }
+  bool hit(const ray& r, interval ray_t) const { return rt_host::slab_overlap(x_, y_, z_, r, ray_t); }  // aabb.h:28-33
 
  private:
   interval x_, y_, z_;

@@ -16,4 +16,8 @@ class interval {
   static interval enclose(interval a, interval b) {
     return interval(a.min < b.min ? a.min : b.min, a.max > b.max ? a.max : b.max);
   }
+  static const interval empty, universe;  // interval.h:32,40-41
 };
+// C++17 inline variables: one definition however many translation units include this header
+inline const interval interval::empty = interval(+infinity, -infinity);
+inline const interval interval::universe = interval(-infinity, +infinity);

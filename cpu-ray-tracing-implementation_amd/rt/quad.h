@@ -19,11 +19,38 @@ class quad : public hittable {
     scene_builder::put3(o.c, v_);
     return sb.emit_object(o);
   }
+  bool hit(const ray& r, interval ray_t, hit_record& rec) const override {  // quad.h:30-64
+    double a, b;
+    const double t = rt_host::quad_root(corner_, u_, v_, unit_normal(), r, ray_t, a, b);
+    if (std::isnan(t)) return false;
+    rec.u = a;
+    rec.v = b;
+    rec.t = t;
+    rec.p = r.at(t);
+    rec.mat = mat_;
+    rec.set_face_normal(r, unit_normal());
+    return true;
+  }
+  aabb get_bounding_box() const override {  // quad.h:19-21: both diagonals
+    return aabb::enclose(aabb(corner_, corner_ + u_ + v_), aabb(corner_ + u_, corner_ + v_));
+  }
+  // quad.h:66-73: solid-angle pdf of a direction that hits the quad from origin, else 0
+  double pdf_value(const point3& origin, const vec3& direction) const override {
+    hit_record rec;
+    if (!hit(ray(origin, direction), interval(0.001, infinity), rec)) return 0;
+    const double dist2 = rec.t * rec.t * direction.length_squared();
+    return dist2 / (std::fabs(dot(unit_vector(direction), rec.normal)) * cross(u_, v_).length());
+  }
+  vec3 random(const point3& origin) const override {  // quad.h:75-78, GCC draws v's coefficient first
+    const double bv = random_double(), bu = random_double();
+    return corner_ + bu * u_ + bv * v_ - origin;
+  }
 
  private:
   point3 corner_;
   vec3 u_, v_;
   std::shared_ptr<material> mat_;
+  vec3 unit_normal() const { return unit_vector(cross(u_, v_)); }
 };
 
 // The six sides of the box spanned by two opposite corners (quad.h:91-112), same order and orientation.

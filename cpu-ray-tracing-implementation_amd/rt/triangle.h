@@ -17,6 +17,23 @@ class triangle : public hittable {
     scene_builder::put3(o.c, p2_);
     return sb.emit_object(o);
   }
+  bool hit(const ray& r, interval ray_t, hit_record& rec) const override {  // triangle.h:30-40 (u, v untouched)
+    const double t = rt_host::triangle_root(p0_, p1_, p2_, r, ray_t);
+    if (std::isnan(t)) return false;
+    rec.t = t;
+    rec.p = r.at(t);
+    rec.set_face_normal(r, unit_vector(cross(p1_ - p0_, p2_ - p0_)));
+    rec.mat = mat_;
+    return true;
+  }
+  aabb get_bounding_box() const override {  // triangle.h:42-48
+    point3 lo, hi;
+    for (int k = 0; k < 3; k++) {
+      lo[k] = std::fmin(p0_[k], std::fmin(p1_[k], p2_[k]));
+      hi[k] = std::fmax(p0_[k], std::fmax(p1_[k], p2_[k]));
+    }
+    return aabb(lo, hi);
+  }
 
  private:
   vec3 p0_, p1_, p2_;

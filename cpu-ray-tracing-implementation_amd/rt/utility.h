@@ -28,3 +28,11 @@ inline vec3 random_vec(double lo, double hi) {
   return vec3(x, y, z);
 }
 inline double clamp(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
+// utility.h:30-42: uniform on (not in) the unit sphere, cos(theta) from the first draw, phi from the second
+inline vec3 random_in_unit_sphere() {
+  const double u_cos = random_double();
+  const double u_phi = random_double();
+  const double ct = 1 - 2 * u_cos, st = std::sqrt(1 - ct * ct), phi = 2 * pi * u_phi;
+  return vec3(st * std::cos(phi), ct, st * std::sin(phi));
+}
+inline vec3 random_unit_vec() { return unit_vector(random_in_unit_sphere()); }  // utility.h:44

@@ -53,4 +53,9 @@ inline vec3 cross(const vec3& a, const vec3& b) {
 inline vec3 unit_vector(const vec3& v) { return v / v.length(); }
 inline vec3 floor(const vec3& v) { return vec3(std::floor(v.x()), std::floor(v.y()), std::floor(v.z())); }
 inline vec3 ceil(const vec3& v) { return vec3(std::ceil(v.x()), std::ceil(v.y()), std::ceil(v.z())); }
+inline vec3 fmod(const vec3& v, const vec3& m) {  // vec3.h:86, per component
+  vec3 r;
+  for (int k = 0; k < 3; k++) r[k] = std::fmod(v[k], m[k]);
+  return r;
+}
 inline vec3 fract(const vec3& v) { return v - floor(v); }

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6
 
 typedef enum rt_status {
   RT_OK = 0,
@@ -234,6 +234,10 @@ typedef struct rt_scene_info {
   uint64_t bytes_f64;
   int32_t flat_quads; /* fp32 flat program (quad/box scenes): world-space axis-aligned quads */
   int32_t flat_boxes; /*   and lambertian boxes traced as one slab test each; 0/0 = none */
+  int32_t wide_nodes; /* fp32 wide BVH (world-level primitives): 4-wide nodes; 0 = none */
+  int32_t wide_stack; /*   stack entries a ray can need in it */
+  int32_t wide_kinds; /*   primitive kinds present: 1 sphere, 2 triangle, 4 quad, 8 moving sphere */
+  int32_t wide_prim_words; /* 16-byte words of its primitive records */
 } rt_scene_info;
 
 typedef struct rt_context rt_context;

@@ -84,11 +84,18 @@ def main():
              "valu_per_launch": valu,
              "valu_issue_frac_measured_clock": round(valu * 2 / (1024 * gui / 8), 4) if gui else None,
              "grbm_gui_active_per_launch": gui,
+             # active lanes per issued VALU instruction (rocprof's VALUUtilization)
+             "valu_lane_util": (round(fam_mean("SQ_THREAD_CYCLES_VALU")[0] / (64 * fam_mean("SQ_ACTIVE_INST_VALU")[0]), 4)
+                                if fam_mean("SQ_THREAD_CYCLES_VALU")[0] and fam_mean("SQ_ACTIVE_INST_VALU")[0] else None),
+             "wait_frac": (round(fam_mean("SQ_WAIT_ANY")[0] / fam_mean("SQ_WAVE_CYCLES")[0], 4)
+                           if fam_mean("SQ_WAIT_ANY")[0] and fam_mean("SQ_WAVE_CYCLES")[0] else None),
              "hbm_bytes_per_launch": traffic["bytes_per_launch"] if fetch and write else None,
              "counters": {c: fam_mean(c)[0] for c in sorted({c for k, cs in acc.items() if k.startswith(fam)
                                                              for c in cs})},
              "formulas": {"valu_issue_frac_measured_clock": "SQ_INSTS_VALU * 2 / (1024 SIMDs * GRBM_GUI_ACTIVE / 8 "
-                                                            "XCDs)", "hbm_bytes": "(2*FETCH_SIZE + WRITE_SIZE) * 1024"},
+                                                            "XCDs)",
+                          "valu_lane_util": "SQ_THREAD_CYCLES_VALU / (64 * SQ_ACTIVE_INST_VALU)",
+                          "wait_frac": "SQ_WAIT_ANY / SQ_WAVE_CYCLES", "hbm_bytes": "(2*FETCH_SIZE + WRITE_SIZE) * 1024"},
              "source": f"{tag}_pmc_summary.csv"}
         with open(os.path.join(out, f"{tag}_pmc.json"), "w") as fh:
             json.dump(d, fh, indent=1)

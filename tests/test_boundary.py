@@ -28,7 +28,7 @@ def test_every_declared_symbol_is_exported():
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(abi.SIGNATURES), set(names) ^ set(abi.SIGNATURES)
-    assert lib.rt_abi_version() == abi.ABI_VERSION == 5
+    assert lib.rt_abi_version() == abi.ABI_VERSION == 6
 
 
 def test_struct_layout_matches_c(tmp_path):
@@ -68,6 +68,24 @@ def test_scene_check_config_scenes(name, quads, spheres, linear, flat):
     assert (info.flat_quads, info.flat_boxes) == flat
     if not linear:
         assert info.bvh_nodes > 0 and 1 <= info.stack_need <= 32
+    # the fp32 wide BVH: only RTOW (a bvh_node of world-level spheres) gets one
+    if name == "rtow":
+        assert info.wide_kinds == 1 and 0 < info.wide_nodes < 339 and 1 <= info.wide_stack <= 32
+        assert info.wide_prim_words == 2 * 339  # [c1, entry] [dc, r] per sphere
+    else:
+        assert info.wide_nodes == 0 and info.wide_kinds == 0
+
+
+def test_scene_check_wide_bvh_needs_world_level_primitives():
+    # a translate/rotate instance under the BVH keeps the binary-BVH traversal (instances carry state)
+    s = SceneBuilder()
+    m = s.lambertian(s.solid((0.5, 0.5, 0.5)))
+    objs = [s.sphere((i, 0, 0), 0.3, m) for i in range(20)]
+    st, info, _ = abi.scene_check(s.desc(s.bvh(objs)))
+    assert st == abi.RT_OK and info.wide_kinds == 1 and info.wide_nodes > 0
+    objs.append(s.translate(s.sphere((0, 0, 0), 0.3, m), (0, 2, 0)))
+    st, info, _ = abi.scene_check(s.desc(s.bvh(objs)))
+    assert st == abi.RT_OK and info.wide_nodes == 0 and info.bvh_nodes > 0
 
 
 def test_scene_check_volume_list_keeps_reference_order():

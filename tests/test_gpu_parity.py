@@ -75,14 +75,18 @@ def test_fp32_device_matches_oracle(ctx, name, w, a, spp, depth):
     assert (rmse(img, ref) < 1e-4).all(), rmse(img, ref)
 
 
-def test_fp32_rtow_statistics(ctx):
-    # specular chains through glass/metal spheres amplify fp32 rounding into different
-    # paths for a few samples; the image statistics still agree with the oracle
-    desc, cam, _, _ = scenes.rtow(width=96, aspect=1.5)
-    img, ref, _ = render_both(ctx, desc, cam, 16, 50, 3, F32)
-    np.testing.assert_allclose(img.reshape(-1, 3).mean(0), ref.reshape(-1, 3).mean(0), rtol=1e-3)
-    assert np.mean(np.abs(img - ref).max(-1) > 1e-3) < 0.005
-    assert (rmse(img, ref) < 2e-3).all(), rmse(img, ref)
+def test_fp32_rtow_matches_oracle_at_config_spp(ctx):
+    # C3 (main.cc:105-153) at its own 512 spp and depth 50 (main.cc:150), 48x32 px: RMSE < 1e-4.
+    # fp32 follows the oracle's fp64 paths sample for sample except where rounding sends a specular
+    # chain through the glass/metal spheres another way; such a sample moves its pixel by ~value/spp,
+    # so the per-pixel error shrinks with spp (at 8 spp RMSE ~7e-4; bench.py's full-C3 rows ~9e-5)
+    desc, cam, _, _ = scenes.rtow(width=48, aspect=1.5)
+    ctx.upload(desc)
+    img = ctx.render(cam, 512, 50, seed=3, precision=F32).astype(np.float64)
+    ref, _ = oracle.render(oracle.from_desc(desc), cam, 512, 50, seed=3, threads=8)
+    np.testing.assert_allclose(img.reshape(-1, 3).mean(0), ref.reshape(-1, 3).mean(0), rtol=1e-4)
+    assert np.mean(np.abs(img - ref).max(-1) > 1e-3) < 0.01
+    assert (rmse(img, ref) < 1e-4).all(), rmse(img, ref)
 
 
 @pytest.mark.parametrize("name,w,a,spp,depth,limit", [
