@@ -397,13 +397,28 @@ __device__ __forceinline__ bool sphere_test(V<R> c1, V<R> dc, R r, bool moving, 
     if (dot(d, o - c) >= R(0)) return false;  // leaving the sphere it starts on
     far_only = true;
   }
-  if (sizeof(R) == 4 && r > R(RT_BIG_SPHERE_R)) {
-    // big spheres (the RTOW ground, r = 1000): |o-c|^2 - r^2 cancels catastrophically in fp32
-    double td;
-    if (!sphere_roots<double>(o.x, o.y, o.z, d.x, d.y, d.z, c.x, c.y, c.z, r, tmin, tmax, far_only, td))
-      return false;
-    t = (R)td;
-    return true;
+  if constexpr (sizeof(R) == 4) {
+    if (r > R(RT_BIG_SPHERE_R)) {
+      // big spheres (the RTOW ground, r = 1000): |o-c|^2 - r^2 cancels catastrophically in fp32 (and
+      // so does the perpendicular-distance discriminant of sphere_roots). Only that quantity is formed
+      // in fp64; then disc = b^2 - a c and the roots q/a, c/q (q = b + sign(b) sqrt(disc)) have no
+      // cancellation left except at a grazing double root.
+      const double gx = (double)o.x - (double)c.x, gy = (double)o.y - (double)c.y, gz = (double)o.z - (double)c.z;
+      const float cc = (float)((gx * gx + gy * gy + gz * gz) - (double)r * (double)r);
+      const float a = d.x * d.x + d.y * d.y + d.z * d.z;
+      const float bh = -(d.x * (float)gx + d.y * (float)gy + d.z * (float)gz);  // -b/2
+      const float disc = bh * bh - a * cc;
+      if (disc < 0.f) return false;
+      const float q = bh + copysignf(fsqrt(disc), bh);
+      const float r0 = fdiv(cc, q), r1 = fdiv(q, a);
+      float root = fminf(r0, r1);
+      if (far_only || !(tmin <= root && root <= tmax)) {
+        root = fmaxf(r0, r1);
+        if (!(tmin <= root && root <= tmax)) return false;
+      }
+      t = root;
+      return true;
+    }
   }
   return sphere_roots<R>(o.x, o.y, o.z, d.x, d.y, d.z, c.x, c.y, c.z, r, tmin, tmax, far_only, t);
 }
@@ -722,11 +737,13 @@ struct WideRay {
   uint32_t e;     // its entry (kNoHit: none)
 };
 // An LDS-resident tree (LDSN) is small: its child codes are rewritten to 16 bits when it is copied
-// into LDS (node index < 2^15, or 0x8000 | (count - 1) << 12 | first word < 2^12), which halves the
-// per-lane stack (uint16 entries) -- the LDS a block needs, and with it the blocks a CU can hold.
+// into LDS -- a node as its LDS offset in 16-byte units (index * 9 < 2^15), a leaf as
+// 0x8000 | (count - 1) << 12 | first word (< 2^12) -- which halves the per-lane stack (uint16
+// entries), and with it the LDS a block needs; the four codes of a node are one 8-byte word.
 constexpr uint32_t kWLeaf16 = 0x8000u;
+constexpr uint32_t kWNodeLdsUnits = kWNodeLdsStride / 16u;
 __host__ __device__ __forceinline__ uint32_t wide_code16(uint32_t c) {
-  return (c & kWLeaf) ? (kWLeaf16 | (((c >> kWCountShift) & 7u) << 12) | (c & 0xFFFu)) : c;
+  return (c & kWLeaf) ? (kWLeaf16 | (((c >> kWCountShift) & 7u) << 12) | (c & 0xFFFu)) : c * kWNodeLdsUnits;
 }
 template <bool LDSN>
 using WStackT = typename std::conditional<LDSN, uint16_t, uint32_t>::type;
@@ -760,8 +777,21 @@ __device__ __forceinline__ bool trace_wide(const DevScene<float>& sc, const unsi
   bool done = false;
   for (;;) {
     while (!(cur & kLeafBit)) {  // inner nodes until this lane holds a leaf (while-while)
-      const float4* nd = LDSN ? (const float4*)(lds_nodes + cur * kWNodeLdsStride) : (const float4*)(sc.wnodes + cur);
+      const float4* nd = LDSN ? (const float4*)(lds_nodes + (cur << 4)) : (const float4*)(sc.wnodes + cur);
       const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
+      // LDS tree: a child's code is loaded when it is pushed (loading all four with the boxes keeps them
+      // live through the slab tests and the sort, which spilled: C3 76.4 -> 81.5 ms/frame). Tree in HBM:
+      // all four come with the boxes, one latency instead of one per push (C4 462 -> 421 ms/frame).
+      uint4 cc{};
+      if constexpr (!LDSN) cc = *(const uint4*)(nd + 6);
+      auto child = [&](uint32_t k) -> uint32_t {
+        if constexpr (LDSN) {
+          return ((const uint16_t*)(nd + 6))[k & 3u];
+        } else {
+          const uint32_t sl = k & 3u;
+          return sl == 0 ? cc.x : (sl == 1 ? cc.y : (sl == 2 ? cc.z : cc.w));
+        }
+      };
       uint32_t k0 = slab(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, 0u);
       uint32_t k1 = slab(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, 1u);
       uint32_t k2 = slab(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, 2u);
@@ -786,11 +816,10 @@ __device__ __forceinline__ bool trace_wide(const DevScene<float>& sc, const unsi
         cur = stk[(--sp) * BLOCK];
         continue;
       }
-      const uint32_t* ch = (const uint32_t*)(nd + 6);
-      if (k3 != 0xFFFFFFFFu) stk[(sp++) * BLOCK] = ch[k3 & 3u];
-      if (k2 != 0xFFFFFFFFu) stk[(sp++) * BLOCK] = ch[k2 & 3u];
-      if (k1 != 0xFFFFFFFFu) stk[(sp++) * BLOCK] = ch[k1 & 3u];
-      cur = ch[k0 & 3u];
+      if (k3 != 0xFFFFFFFFu) stk[(sp++) * BLOCK] = child(k3);
+      if (k2 != 0xFFFFFFFFu) stk[(sp++) * BLOCK] = child(k2);
+      if (k1 != 0xFFFFFFFFu) stk[(sp++) * BLOCK] = child(k1);
+      cur = child(k0);
     }
     if (done) break;
     uint32_t w = LDSN ? (cur & 0xFFFu) : (cur & kWFirstMask);

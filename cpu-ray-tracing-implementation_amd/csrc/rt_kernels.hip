@@ -444,48 +444,31 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
         if constexpr (sizeof(R) == 8) {
           outward = (po - ld3(sp.cn)) / sp.r;
         } else {
-          if (sp.r > R(RT_BIG_SPHERE_R)) {
-            // Big spheres (intersected in fp64, see sphere_test): o + t*d in fp32 is off the
-            // surface by ~1e-7 absolute, enough to flip the sign of y near the top of the RTOW
-            // ground (y = 0 under the glass sphere) and with it the checker parity
-            // (texture.h:51-55). Rebuild the point on the sphere in fp64, then round.
-            double cx = sp.c1[0], cy = sp.c1[1], cz = sp.c1[2];
-            if (sp.moving) {
-              cx += (double)s.tm * sp.dc[0];
-              cy += (double)s.tm * sp.dc[1];
-              cz += (double)s.tm * sp.dc[2];
-            }
-            double vx = (double)oo.x + (double)t * dd.x - cx, vy = (double)oo.y + (double)t * dd.y - cy,
-                   vz = (double)oo.z + (double)t * dd.z - cz;
-            double k = (double)sp.r / sqrt(vx * vx + vy * vy + vz * vz);
-            po = mkv((float)(cx + vx * k), (float)(cy + vy * k), (float)(cz + vz * k));
-            outward = (po - ld3(sp.cn)) * fdiv(R(1), sp.r);
-          } else {
 #if RT_SPHERE_REFINE
-            // The hit re-solved in fp64 from the fp32 ray (the root nearest the fp32 t), and the
-            // point and normal (sphere.h:67-69) built from it: the fp32 root is ~1e-6 off along
-            // the ray for t ~ 10, which tilts a small sphere's normal by ~1e-5 -- enough for a
-            // chain of mirror / glass bounces to leave the fp64 path a few times per million
-            // segments. This costs one fp64 quadratic per sphere hit.
-            const double cx = (double)sp.c1[0] + (double)s.tm * sp.dc[0], cy = (double)sp.c1[1] + (double)s.tm * sp.dc[1],
-                         cz = (double)sp.c1[2] + (double)s.tm * sp.dc[2];
-            const double ox = oo.x, oy = oo.y, oz = oo.z, dx = dd.x, dy = dd.y, dz = dd.z;
-            const double fx = ox - cx, fy = oy - cy, fz = oz - cz, rr = sp.r;
-            const double a = dx * dx + dy * dy + dz * dz, bh = dx * fx + dy * fy + dz * fz;
-            const double disc = bh * bh - a * ((fx * fx + fy * fy + fz * fz) - rr * rr);
-            double td = t;
-            if (disc >= 0) {
-              const double ia = 1.0 / a, sq = sqrt(disc);
-              const double t0 = (-bh - sq) * ia, t1 = (-bh + sq) * ia;
-              td = fabs(t0 - (double)t) <= fabs(t1 - (double)t) ? t0 : t1;
-            }
-            const double px = ox + td * dx, py = oy + td * dy, pz = oz + td * dz, ir = 1.0 / rr;
-            po = mkv((float)px, (float)py, (float)pz);
-            outward = mkv((float)((px - sp.cn[0]) * ir), (float)((py - sp.cn[1]) * ir), (float)((pz - sp.cn[2]) * ir));
+          // The hit refined in fp64 from the fp32 ray: one Newton step on the quadratic
+          // g(t) = a t^2 + 2 b t + c from the fp32 root (which is ~1e-7 relative off: ~1e-6 along
+          // the ray for t ~ 10, tilting a small sphere's normal by ~1e-5 -- enough for a chain of
+          // mirror / glass bounces to leave the fp64 path a few times per million segments),
+          // then the point and normal (sphere.h:67-69) from the refined root. A step that does
+          // not land near the fp32 root (a grazing double root) keeps it.
+          const double cx = (double)sp.c1[0] + (double)s.tm * sp.dc[0], cy = (double)sp.c1[1] + (double)s.tm * sp.dc[1],
+                       cz = (double)sp.c1[2] + (double)s.tm * sp.dc[2];
+          const double ox = oo.x, oy = oo.y, oz = oo.z, dx = dd.x, dy = dd.y, dz = dd.z;
+          const double fx = ox - cx, fy = oy - cy, fz = oz - cz, rr = sp.r;
+          const double a = dx * dx + dy * dy + dz * dz, b = dx * fx + dy * fy + dz * fz;
+          const double c = (fx * fx + fy * fy + fz * fz) - rr * rr, t0 = t;
+          const double at = a * t0 + b;
+          double td = t0 - ((at + b) * t0 + c) / (2.0 * at);
+          if (!(fabs(td - t0) <= 1e-4 * fabs(t0))) td = t0;
+          const double px = ox + td * dx, py = oy + td * dy, pz = oz + td * dz;
+          po = mkv((float)px, (float)py, (float)pz);
+          outward = mkv((float)(px - sp.cn[0]), (float)(py - sp.cn[1]), (float)(pz - sp.cn[2])) * fdiv(R(1), sp.r);
 #else
-            outward = (po - ld3(sp.cn)) * fdiv(R(1), sp.r);
+          outward = (po - ld3(sp.cn)) * fdiv(R(1), sp.r);
 #endif
-          }
+          // big spheres (the RTOW ground, r = 1000) in particular: o + t*d in fp32 is off the surface
+          // by ~1e-7 absolute, enough to flip the sign of y near the top of the ground (y = 0 under the
+          // glass sphere) and with it the checker parity (texture.h:51-55)
         }
         mat = sp.mat;
         if constexpr (CAMX) sphere_uv(outward, hu, hv);  // sphere.h:70
@@ -718,7 +701,8 @@ struct WideTrav {
       for (uint32_t j = threadIdx.x; j < sc.n_wnodes * 7u; j += kBlock) {
         const uint32_t nd = j / 7u, f = j - nd * 7u;
         uint4 v = gn[nd * 8u + f];
-        if (f == 6) v = make_uint4(wide_code16(v.x), wide_code16(v.y), wide_code16(v.z), wide_code16(v.w));
+        if (f == 6)  // four 16-bit codes in the first 8 bytes (trace_wide)
+          v = make_uint4(wide_code16(v.x) | wide_code16(v.y) << 16, wide_code16(v.z) | wide_code16(v.w) << 16, 0u, 0u);
         *(uint4*)(base + nd * kWNodeLdsStride + f * 16u) = v;
       }
       uint4* pw = (uint4*)(base + sc.n_wnodes * kWNodeLdsStride);
@@ -1274,8 +1258,8 @@ inline size_t wide_lds_bytes(const DevScene<float>& sc, bool ldsn) {
 template <bool SPH, bool TRI, bool QUAD, bool MOV>
 void launch_wide_k(const Params<float>& p, uint32_t grid, hipStream_t st) {
   const size_t full = wide_lds_bytes(p.sc, true);
-  // LDS-resident trees use 16-bit child codes (wide_code16): node index < 2^15, first word < 2^12
-  if (full <= kWideLdsBudget && p.sc.n_wnodes < 0x8000u && p.sc.n_wprim_words <= 0x1000u)
+  // LDS-resident trees use 16-bit child codes (wide_code16): node offset (index x 9) < 2^15, first word < 2^12
+  if (full <= kWideLdsBudget && p.sc.n_wnodes * kWNodeLdsUnits < 0x8000u && p.sc.n_wprim_words <= 0x1000u)
     launch_one(k_persist_occ<float, WideTrav<SPH, TRI, QUAD, MOV, true>, false>, p, grid, st, full);
   else
     launch_one(k_persist_occ<float, WideTrav<SPH, TRI, QUAD, MOV, false>, false>, p, grid, st,
