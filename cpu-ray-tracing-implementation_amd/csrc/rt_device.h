@@ -236,7 +236,12 @@ struct DevScene {
   const float4* wprims;
   uint32_t n_wnodes, n_wprim_words, wroot, wide_stack, wide_kinds;
   int32_t has_wide;
+  // a tree in HBM keeps at most kWideLdsStack stack entries per lane in LDS; deeper entries (rare:
+  // every child of every node on a path hit) go to wide_spill[(depth - kWideLdsStack) * spill_lanes + lane]
+  uint32_t* wide_spill;
+  uint32_t spill_lanes;
 };
+constexpr uint32_t kWideLdsStack = 24;
 
 // World -> object through an instance chain (hittable.h:75-82, 125-135, 192-202, 259-270).
 template <class R>
@@ -764,6 +769,20 @@ __device__ __forceinline__ bool trace_wide(const DevScene<float>& sc, const unsi
   int sp = ry.sp;
   float tmax = ry.tmax;
   uint32_t e_best = ry.e;
+  // the lane's stack: LDS, and for a tree in HBM its spill area past kWideLdsStack entries
+  [[maybe_unused]] const uint32_t lane = blockIdx.x * BLOCK + threadIdx.x;
+  auto push = [&](uint32_t v) {
+    if (LDSN || sp < (int)kWideLdsStack)
+      stk[sp * BLOCK] = (WStackT<LDSN>)v;
+    else
+      sc.wide_spill[(uint32_t)(sp - (int)kWideLdsStack) * sc.spill_lanes + lane] = v;
+    sp++;
+  };
+  auto pop = [&]() -> uint32_t {
+    --sp;
+    if (LDSN || sp < (int)kWideLdsStack) return stk[sp * BLOCK];
+    return sc.wide_spill[(uint32_t)(sp - (int)kWideLdsStack) * sc.spill_lanes + lane];
+  };
   auto slab = [&](float lx, float ly, float lz, float hx, float hy, float hz, uint32_t c) {
     const float tx0 = (lx - o.x) * inv.x, tx1 = (hx - o.x) * inv.x;
     const float ty0 = (ly - o.y) * inv.y, ty1 = (hy - o.y) * inv.y;
@@ -813,12 +832,12 @@ __device__ __forceinline__ bool trace_wide(const DevScene<float>& sc, const unsi
           done = true;
           break;
         }
-        cur = stk[(--sp) * BLOCK];
+        cur = pop();
         continue;
       }
-      if (k3 != 0xFFFFFFFFu) stk[(sp++) * BLOCK] = child(k3);
-      if (k2 != 0xFFFFFFFFu) stk[(sp++) * BLOCK] = child(k2);
-      if (k1 != 0xFFFFFFFFu) stk[(sp++) * BLOCK] = child(k1);
+      if (k3 != 0xFFFFFFFFu) push(child(k3));
+      if (k2 != 0xFFFFFFFFu) push(child(k2));
+      if (k1 != 0xFFFFFFFFu) push(child(k1));
       cur = child(k0);
     }
     if (done) break;
@@ -852,7 +871,7 @@ __device__ __forceinline__ bool trace_wide(const DevScene<float>& sc, const unsi
       done = true;
       break;
     }
-    cur = stk[(--sp) * BLOCK];
+    cur = pop();
     if constexpr (PAUSE < 64) {
       if ((uint32_t)__popcll(__ballot(1)) <= keep_going) break;  // enough of the wave waits to be shaded
     }

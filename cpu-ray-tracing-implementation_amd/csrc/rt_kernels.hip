@@ -1061,6 +1061,7 @@ struct rt_context {
   bool has_scene = false;
   DevBuf scene32, scene64;
   DevBuf state, partial, pixmap, queue0, queue1, blk, out_tmp, counters, camx, heads, tiles;
+  DevBuf wide_spill;  // the wide traversal's stack entries past kWideLdsStack (deep trees in HBM)
   CamDev cam_host;  // source of camx (kept alive for the async copy)
   uint32_t* total_host = nullptr;  // pinned: [0] live slots, [1] fault word, [16..] segment counter shards
   uint64_t samples = 0;
@@ -1252,7 +1253,9 @@ void launch_one(KernelT kern, Params<R> p, uint32_t grid, hipStream_t st, size_t
 // Dynamic LDS of a wide-BVH launch: the whole tree when it fits the budget (LDSN), else the stack only.
 constexpr size_t kWideLdsBudget = 40u << 10;  // bytes per 256-lane block: 4 blocks per CU of 160 KiB
 inline size_t wide_lds_bytes(const DevScene<float>& sc, bool ldsn) {
-  const size_t stack = (size_t)sc.wide_stack * kBlock * (ldsn ? 2u : 4u);  // uint16 entries in an LDS tree
+  // an LDS tree: every entry in LDS, uint16; a tree in HBM: up to kWideLdsStack uint32 entries (the rest spill)
+  const size_t stack = ldsn ? (size_t)sc.wide_stack * kBlock * 2u
+                            : (size_t)std::min<uint32_t>(sc.wide_stack, kWideLdsStack) * kBlock * 4u;
   return (ldsn ? (size_t)sc.n_wnodes * kWNodeLdsStride + (size_t)sc.n_wprim_words * 16u : 0u) + stack;
 }
 template <bool SPH, bool TRI, bool QUAD, bool MOV>
@@ -1261,8 +1264,9 @@ void launch_wide_k(const Params<float>& p, uint32_t grid, hipStream_t st) {
   // LDS-resident trees use 16-bit child codes (wide_code16): node offset (index x 9) < 2^15, first word < 2^12
   if (full <= kWideLdsBudget && p.sc.n_wnodes * kWNodeLdsUnits < 0x8000u && p.sc.n_wprim_words <= 0x1000u)
     launch_one(k_persist_occ<float, WideTrav<SPH, TRI, QUAD, MOV, true>, false>, p, grid, st, full);
-  else
-    launch_one(k_persist_occ<float, WideTrav<SPH, TRI, QUAD, MOV, false>, false>, p, grid, st,
+  else  // the spill area holds spill_lanes lanes: never launch more (the resident grid is below it)
+    launch_one(k_persist_occ<float, WideTrav<SPH, TRI, QUAD, MOV, false>, false>, p,
+               p.sc.wide_spill ? std::min<uint32_t>(grid, p.sc.spill_lanes / kBlock) : grid, st,
                wide_lds_bytes(p.sc, false));
 }
 // Kernel for the primitive kinds of the scene: spheres only (RTOW), triangles only (meshes), or all.
@@ -1425,6 +1429,15 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     unsigned char* sp = (unsigned char*)c->state.ptr;
     Params<R> p{};
     p.sc = dev_scene<R>(hdr, sbase);
+    if (!f64 && hdr.has_wide && hdr.wide_stack > kWideLdsStack) {
+      // a deep wide tree: a spill area of (need - kWideLdsStack) entries for every lane the chip can hold
+      int ncu = 0;
+      RT_HIP(c, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
+      const uint32_t lanes = (uint32_t)std::max(ncu, 1) * 2048u;  // 32 waves of 64 per CU at most
+      if ((s = ensure(c, c->wide_spill, 4ull * (hdr.wide_stack - kWideLdsStack) * lanes)) != RT_OK) return s;
+      p.sc.wide_spill = (uint32_t*)c->wide_spill.ptr;
+      p.sc.spill_lanes = lanes;
+    }
     if (prm->traversal == RT_TRAV_ORDERED) p.sc.has_flat = p.sc.has_wide = 0;
     p.O = (R4<R>*)sp;
     p.D = (R4<R>*)(sp + r4);
@@ -1605,7 +1618,7 @@ void rt_context_destroy(rt_context* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (DevBuf* b : {&c->scene32, &c->scene64, &c->state, &c->partial, &c->pixmap, &c->queue0, &c->queue1, &c->blk,
+  for (DevBuf* b : {&c->scene32, &c->scene64, &c->state, &c->partial, &c->pixmap, &c->queue0, &c->queue1, &c->blk, &c->wide_spill,
                     &c->out_tmp, &c->counters, &c->camx, &c->heads, &c->tiles, &c->fault})
     if (b->ptr) (void)hipFree(b->ptr);
   for (hipEvent_t e : c->events) (void)hipEventDestroy(e);

@@ -19,6 +19,8 @@
 #include <string>
 #include <unordered_map>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <limits>
@@ -1165,8 +1167,11 @@ bool Compiler::wide_bvh(const std::vector<Item>& prims, CompiledScene* out) {
   };
   uint32_t root;
   int need;
-  if (!emit(0, root, need)) return false;
-  if (need > kStackDepth) return false;
+  const bool ok = emit(0, root, need);
+  if (std::getenv("RT_DEBUG_WIDE"))
+    std::fprintf(stderr, "[wide] ok %d need %d nodes %zu words %zu binary nodes %zu\n", (int)ok, need, wn.size(),
+                 words.size(), bn.size());
+  if (!ok || need > kWideStackMax) return false;
   SceneHeader& h = out->hdr;
   h.off_wnodes = append(out->blob32, wn);
   h.off_wprims = append(out->blob32, words);

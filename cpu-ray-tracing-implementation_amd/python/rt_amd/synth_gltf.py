@@ -1,12 +1,20 @@
-"""glTF 2.0 writer and the synthetic Sponza stand-in.
+"""glTF 2.0 writer and the synthetic Sponza stand-ins.
 
 The reference's C4 workload renders Sponza (main.cc:439-498) from
-./assets/Sponza/glTF/Sponza.gltf, which is not shipped with it (and there is no
-network here). `write_sponza_standin` writes a procedural atrium of the same size
--- 262,267 triangles: floor, side walls with a gallery, two rows of columns --
-placed where main.cc's camera (500, 320, 90) -> (0, 280, 0) and light quad
-(0, 1200, 0) + 500 x 500 see it, as a glTF whose last mesh holds the triangles in
-uint16-indexed primitives (the only index type main.cc reads).
+./assets/Sponza/glTF/Sponza.gltf. The reference ships that file but not its
+Sponza.bin (9,528,220 bytes of vertex and index data), and there is no network here.
+
+`write_sponza_standin` keeps the real Sponza.gltf (a copy of the reference's file is
+under tests/golden/assets/Sponza/glTF) and writes a Sponza.bin that fills its layout:
+the same 103 primitives of the last mesh, the same accessors, offsets and uint16 index
+buffers (shared between primitives where the real file shares them), 262,267 triangles.
+Each primitive's vertices form a planar grid spanning the two largest extents of its
+accessor's min/max box at the box's centre, so the geometry sits where Sponza's objects
+sit, with their triangle counts. Cells are split along one diagonal, then (only when a
+primitive has more triangles than cells) along the other: coplanar duplicates shade
+identically, so exact-t ties between them do not change an image.
+
+`write_atrium_standin` is the earlier procedural atrium (floor, walls, gallery, columns).
 """
 import json
 import math
@@ -119,8 +127,80 @@ def sponza_standin_pieces():
     return pieces
 
 
-def write_sponza_standin(directory):
-    """Writes <directory>/Sponza.gltf + Sponza.bin; returns the .gltf path."""
+SPONZA_LAYOUT = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))),
+                             "tests", "golden", "assets", "Sponza", "glTF", "Sponza.gltf")
+
+
+def _layout_grid(nv, ntri):
+    """(nx, ny, triangles (ntri, 3)) of a planar nx x ny grid with nx * ny <= nv vertices."""
+    nx = max(2, int(math.isqrt(nv)))
+    ny = max(2, nv // nx)
+    while nx * ny > nv and ny > 2:
+        ny -= 1
+    if nx * ny > nv:
+        raise ValueError(f"a primitive of {nv} vertices is too small for a grid")
+    I, J = np.meshgrid(np.arange(nx - 1), np.arange(ny - 1), indexing="ij")
+    a, b = I * ny + J, (I + 1) * ny + J
+    c, d = b + 1, a + 1
+    first = np.concatenate([np.stack([a, b, c], -1).reshape(-1, 3), np.stack([a, c, d], -1).reshape(-1, 3)])
+    second = np.concatenate([np.stack([a, b, d], -1).reshape(-1, 3), np.stack([b, c, d], -1).reshape(-1, 3)])
+    tris = np.concatenate([first, second])
+    if ntri > len(tris):
+        raise ValueError(f"{ntri} triangles do not fit a grid of {nv} vertices")
+    return nx, ny, tris[:ntri]
+
+
+def write_sponza_standin(directory, layout=SPONZA_LAYOUT):
+    """Writes <directory>/Sponza.gltf (the real file) + a Sponza.bin filling its layout; returns the .gltf path.
+    Without the layout file, the procedural atrium."""
+    if not os.path.exists(layout):
+        return write_atrium_standin(directory)
+    os.makedirs(directory, exist_ok=True)
+    with open(layout) as f:
+        doc = json.load(f)
+    acc, views = doc["accessors"], doc["bufferViews"]
+    buf = np.zeros(doc["buffers"][0]["byteLength"], np.uint8)
+
+    def span(a, elem):
+        v = views[acc[a]["bufferView"]]
+        off = v.get("byteOffset", 0) + acc[a].get("byteOffset", 0)
+        return off, acc[a]["count"], elem
+
+    prims = doc["meshes"][-1]["primitives"]  # the loader keeps the last mesh (gltf_loader.h:300-302)
+    groups = {}  # index span -> primitives sharing it
+    for p in prims:
+        groups.setdefault(span(p["indices"], 2)[:2], []).append(p)
+    for (ioff, icount), members in groups.items():
+        nv = min(acc[p["attributes"]["POSITION"]]["count"] for p in members)
+        nx, ny, tris = _layout_grid(nv, icount // 3)
+        idx = np.zeros(icount, np.uint16)
+        idx[: 3 * len(tris)] = tris.reshape(-1)
+        buf[ioff: ioff + 2 * icount] = np.frombuffer(idx.tobytes(), np.uint8)
+        for p in members:
+            pa = p["attributes"]["POSITION"]
+            lo, hi = np.array(acc[pa]["min"], float), np.array(acc[pa]["max"], float)
+            ext = hi - lo
+            u_ax, v_ax = [int(k) for k in np.argsort(-ext)[:2]]
+            s = np.linspace(0.0, 1.0, nx)
+            t = np.linspace(0.0, 1.0, ny)
+            S, T = np.meshgrid(s, t, indexing="ij")
+            pos = np.tile((lo + hi) / 2, (acc[pa]["count"], 1))
+            g = np.tile((lo + hi) / 2, (nx * ny, 1))
+            g[:, u_ax] = lo[u_ax] + S.reshape(-1) * ext[u_ax]
+            g[:, v_ax] = lo[v_ax] + T.reshape(-1) * ext[v_ax]
+            pos[: nx * ny] = g
+            poff, pcount, _ = span(pa, 12)
+            buf[poff: poff + 12 * pcount] = np.frombuffer(pos.astype(np.float32).tobytes(), np.uint8)
+    with open(os.path.join(directory, doc["buffers"][0]["uri"]), "wb") as f:
+        f.write(buf.tobytes())
+    path = os.path.join(directory, "Sponza.gltf")
+    with open(path, "w") as f:
+        json.dump(doc, f)
+    return path
+
+
+def write_atrium_standin(directory):
+    """Writes <directory>/Sponza.gltf + Sponza.bin (the procedural atrium); returns the .gltf path."""
     os.makedirs(directory, exist_ok=True)
     prims, verts, tris = [], [], []
 
