@@ -1,20 +1,23 @@
 // image.h -- image loading for picture_texture (reference: src/image.h:9-117).
 //
 // The reference decodes files with stb_image (stbi_loadf: 8-bit formats come back linear, as
-// (byte / 255)^2.2) or tinyexr, then stores bytes with float_to_byte (<= 0 -> 0, >= 1 -> 255,
-// else int(256 v)). Neither decoder ships in this build, so files are read here in the formats
-// this project writes and reads itself: binary/ASCII PPM (P6/P3, 8-bit, converted to linear like
-// stbi_loadf) and PFM (linear floats). Other hosts decode elsewhere and pass linear floats to
-// image(width, height, pixels). As in the reference, a file that cannot be loaded prints an error
-// and leaves a 0 x 0 image, which picture_texture samples as magenta.
+// powf(byte / 255, 2.2)) or tinyexr, then stores bytes with float_to_byte (<= 0 -> 0, >= 1 -> 255,
+// else int(256 v)). Here: baseline JPEG through our own decoder (rt/jpeg.h, byte-identical to the
+// reference's stb_image on the reference's earthmap.jpg), binary/ASCII PPM (P6/P3, 8-bit) and PFM
+// (linear floats). PNG, EXR and progressive JPEG are not decoded; other hosts decode elsewhere and
+// pass linear floats to image(width, height, pixels). As in the reference, a file that cannot be
+// loaded prints an error and leaves a 0 x 0 image, which picture_texture samples as magenta.
 #pragma once
 #include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <fstream>
 #include <iostream>
+#include <iterator>
 #include <string>
 #include <vector>
+
+#include "jpeg.h"
 
 class image {
  public:
@@ -72,9 +75,24 @@ class image {
     }
     return !t.empty();
   }
+  // stbi__ldr_to_hdr: powf(byte / 255.0f, 2.2f), float all the way
+  static float ldr_to_linear(int v) { return (float)std::pow((float)v / 255.0f, 2.2f); }
   bool load(const std::string& path) {
     std::ifstream in(path, std::ios::binary);
     if (!in) return false;
+    if (in.peek() == 0xFF) {  // JPEG (SOI = FF D8)
+      std::vector<uint8_t> file((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+      rt_jpeg::Image im;
+      std::string err;
+      if (!rt_jpeg::decode(file, im, &err)) {
+        std::cerr << "JPEG: " << err << "\n";
+        return false;
+      }
+      std::vector<float> f(im.rgb.size());
+      for (size_t i = 0; i < f.size(); i++) f[i] = ldr_to_linear(im.rgb[i]);
+      set(im.width, im.height, f);
+      return !bytes_.empty();
+    }
     std::string magic, sw, sh, smax;
     if (!token(in, magic)) return false;
     if (magic == "PF") {  // PFM: linear floats, rows bottom to top, the scale's sign is the byte order
@@ -108,7 +126,7 @@ class image {
         if (!token(in, t)) return false;
         v = std::stoi(t);
       }
-      f[i] = (float)std::pow((double)v / maxv, 2.2);  // stbi_loadf's LDR -> linear conversion
+      f[i] = maxv == 255 ? ldr_to_linear(v) : (float)std::pow((float)v / (float)maxv, 2.2f);
     }
     set(w, h, f);
     return !bytes_.empty();

@@ -311,6 +311,18 @@ def test_picture_textures_match_oracle(ctx, name, tmp_path, monkeypatch):
     np.testing.assert_allclose(img32.reshape(-1, 3).mean(0), ref.reshape(-1, 3).mean(0), rtol=1e-2)
 
 
+def test_reference_earthmap_texture_matches_oracle(ctx, monkeypatch):
+    # main.cc:185-196 with the reference's own earthmap.jpg (decoded by rt/jpeg.h, byte-identical to its
+    # stb_image: tests/test_jpeg.py) on the moving sphere, the missing bathroom.exr skybox magenta
+    monkeypatch.setenv("RT_ASSETS", os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "assets"))
+    cs = plugin.ConfigScene("skybox_and_motion_blur", 48)
+    assert cs.desc.num_image_data == 1024 * 512 * 3
+    img, ref, _ = render_both(ctx, cs.desc, cs.cam, 4, 5, 3, F64)
+    assert np.all(np.abs(img - ref) <= 1e-9 * np.maximum(1.0, np.abs(ref))), np.abs(img - ref).max()
+    img32, _, _ = render_both(ctx, cs.desc, cs.cam, 4, 5, 3, F32)
+    np.testing.assert_allclose(img32.reshape(-1, 3).mean(0), ref.reshape(-1, 3).mean(0), rtol=1e-2)
+
+
 def test_picture_texture_on_quads_matches_oracle(ctx):
     # quad uv = (alpha, beta) (quad.h:58-64), inside a rotated instance, plus a textured sphere
     s = SceneBuilder()
