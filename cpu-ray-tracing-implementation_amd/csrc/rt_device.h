@@ -236,6 +236,7 @@ struct DevScene {
   const float4* wprims;
   uint32_t n_wnodes, n_wprim_words, wroot, wide_stack, wide_kinds;
   int32_t has_wide;
+  uint32_t wide_big;  // primitives at the head of the word stream, tested before the tree
   // a tree in HBM keeps at most kWideLdsStack stack entries per lane in LDS; deeper entries (rare:
   // every child of every node on a path hit) go to wide_spill[(depth - kWideLdsStack) * spill_lanes + lane]
   uint32_t* wide_spill;
@@ -740,6 +741,7 @@ struct WideRay {
   int32_t sp;     // entries on the LDS stack
   float tmax;     // closest hit so far
   uint32_t e;     // its entry (kNoHit: none)
+  uint32_t fresh; // 1: the head primitives (DevScene::wide_big) are still to be tested
 };
 // An LDS-resident tree (LDSN) is small: its child codes are rewritten to 16 bits when it is copied
 // into LDS -- a node as its LDS offset in 16-byte units (index * 9 < 2^15), a leaf as
@@ -793,6 +795,38 @@ __device__ __forceinline__ bool trace_wide(const DevScene<float>& sc, const unsi
     // tn >= tmin > 0: the bit pattern orders like the value; the low 2 bits carry the slot
     return tn <= tf ? ((__float_as_uint(tn) & ~3u) | c) : 0xFFFFFFFFu;
   };
+  // the primitives of a leaf (or of the head list), their records from word w on
+  auto test_prims = [&](uint32_t w, uint32_t count) {
+    for (uint32_t n = count; n > 0; n--) {
+      const float4 h = prims[w];
+      const uint32_t e = __float_as_uint(h.w);
+      const uint32_t ty = etype(e);
+      float th;
+      bool hit = false;
+      if (SPH && (!(TRI || QUAD) || ty == E_SPHERE)) {
+        const float4 b = prims[w + 1];
+        w += 2;
+        hit = sphere_test(mkv(h.x, h.y, h.z), mkv(b.x, b.y, b.z), b.w, MOV, o, d, time, tmin, tmax, e == excl_e, th);
+      } else if (TRI && (!QUAD || ty == E_TRI)) {
+        const float4 a = prims[w + 1], b = prims[w + 2];
+        w += 3;
+        hit = e != excl_e && tri_test(mkv(h.x, h.y, h.z), mkv(a.x, a.y, a.z), mkv(b.x, b.y, b.z), o, d, tmin, tmax, th);
+      } else if (QUAD) {
+        const float4 nD = prims[w + 1], qa = prims[w + 2], qb = prims[w + 3];
+        w += 4;
+        hit = e != excl_e && quad_test(mkv(nD.x, nD.y, nD.z), nD.w, mkv(h.x, h.y, h.z), mkv(qa.x, qa.y, qa.z),
+                                       mkv(qb.x, qb.y, qb.z), o, d, tmin, tmax, th);
+      }
+      if (hit) {
+        tmax = th;
+        e_best = e;
+      }
+    }
+  };
+  if (ry.fresh) {  // every lane alike: no divergence, and the tree starts bounded by their hit
+    test_prims(0u, sc.wide_big);
+    ry.fresh = 0;
+  }
   bool done = false;
   for (;;) {
     while (!(cur & kLeafBit)) {  // inner nodes until this lane holds a leaf (while-while)
@@ -841,32 +875,8 @@ __device__ __forceinline__ bool trace_wide(const DevScene<float>& sc, const unsi
       cur = child(k0);
     }
     if (done) break;
-    uint32_t w = LDSN ? (cur & 0xFFFu) : (cur & kWFirstMask);
-    for (uint32_t n = (LDSN ? ((cur >> 12) & 7u) : ((cur >> kWCountShift) & 63u)) + 1u; n > 0; n--) {
-      const float4 h = prims[w];
-      const uint32_t e = __float_as_uint(h.w);
-      const uint32_t ty = etype(e);
-      float th;
-      bool hit = false;
-      if (SPH && (!(TRI || QUAD) || ty == E_SPHERE)) {
-        const float4 b = prims[w + 1];
-        w += 2;
-        hit = sphere_test(mkv(h.x, h.y, h.z), mkv(b.x, b.y, b.z), b.w, MOV, o, d, time, tmin, tmax, e == excl_e, th);
-      } else if (TRI && (!QUAD || ty == E_TRI)) {
-        const float4 a = prims[w + 1], b = prims[w + 2];
-        w += 3;
-        hit = e != excl_e && tri_test(mkv(h.x, h.y, h.z), mkv(a.x, a.y, a.z), mkv(b.x, b.y, b.z), o, d, tmin, tmax, th);
-      } else if (QUAD) {
-        const float4 nD = prims[w + 1], qa = prims[w + 2], qb = prims[w + 3];
-        w += 4;
-        hit = e != excl_e && quad_test(mkv(nD.x, nD.y, nD.z), nD.w, mkv(h.x, h.y, h.z), mkv(qa.x, qa.y, qa.z),
-                                       mkv(qb.x, qb.y, qb.z), o, d, tmin, tmax, th);
-      }
-      if (hit) {
-        tmax = th;
-        e_best = e;
-      }
-    }
+    test_prims(LDSN ? (cur & 0xFFFu) : (cur & kWFirstMask),
+               (LDSN ? ((cur >> 12) & 7u) : ((cur >> kWCountShift) & 63u)) + 1u);
     if (sp == 0) {
       done = true;
       break;

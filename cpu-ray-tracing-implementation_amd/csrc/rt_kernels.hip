@@ -843,7 +843,7 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
       // resumable traversal: a ray paused with the wave's laggards carries on after the others shade
       using StackT = typename Trav::StackT;
       const uint32_t root = Trav::root(p.sc);
-      WideRay ry{root, 0, Num<float>::inf(), kNoHit};
+      WideRay ry{root, 0, Num<float>::inf(), kNoHit, 1u};
 #pragma unroll 1
       for (;;) {
         if (!Trav::steps(p.sc, trav_nodes, s, (StackT*)wstk, ry)) continue;
@@ -853,7 +853,7 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
         }
         const float t = ry.tmax;
         const uint32_t e = ry.e;
-        ry = WideRay{root, 0, Num<float>::inf(), kNoHit};
+        ry = WideRay{root, 0, Num<float>::inf(), kNoHit, 1u};
         if (!shade<R, CAMX, false>(p, s, t, e, -1, 0)) break;
       }
     } else {
@@ -1209,6 +1209,7 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
   s.wroot = h.wroot;
   s.wide_stack = h.wide_stack;
   s.wide_kinds = h.wide_kinds;
+  s.wide_big = h.wide_big;
   return s;
 }
 
@@ -1665,6 +1666,7 @@ rt_status rt_scene_check(const rt_scene_desc* desc, rt_scene_info* info, char* e
     info->wide_stack = cs.hdr.has_wide ? (int32_t)cs.hdr.wide_stack : 0;
     info->wide_kinds = cs.hdr.has_wide ? (int32_t)cs.hdr.wide_kinds : 0;
     info->wide_prim_words = cs.hdr.has_wide ? (int32_t)cs.hdr.n_wprim_words : 0;
+    info->wide_big = cs.hdr.has_wide ? (int32_t)cs.hdr.wide_big : 0;
     info->spheres = (int32_t)h.n_spheres;
     info->triangles = (int32_t)h.n_tris;
     info->instances = h.num_instances;

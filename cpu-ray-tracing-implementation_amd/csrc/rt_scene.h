@@ -273,6 +273,8 @@ struct SceneHeader {
   uint32_t wide_stack;   // traversal stack entries a lane can need
   uint32_t wide_kinds;   // WK_* bits
   uint32_t has_wide;
+  uint32_t wide_big;     // primitives at the head of the word stream tested before the tree (huge boxes)
+  uint32_t wide_pad_[3];
 };
 
 }  // namespace rtd

@@ -973,7 +973,23 @@ bool Compiler::flat_program(const std::vector<uint32_t>& lin, std::vector<FlatQu
 // tree, collapsed into 4-wide nodes by repeatedly opening the child of largest surface area.
 // Leaves hold their primitives' records in leaf order (no reference list). Closest hits do not
 // depend on the tree except on exact-t ties, as for the binary BVH.
-bool Compiler::wide_bvh(const std::vector<Item>& prims, CompiledScene* out) {
+bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
+  // Primitives whose box covers a large part of the scene (the RTOW ground sphere, r = 1000) would
+  // sit in a leaf that almost every ray reaches, beside leaves of small primitives whose tests
+  // diverge from it. They are tested first, by every lane alike, before the tree (whose traversal
+  // then starts with their hit distance as its bound).
+  std::vector<Item> prims, big;
+  {
+    Box scene;
+    for (const Item& it : all) scene.grow(it.box);
+    const double sa = scene.area();
+    for (const Item& it : all)
+      (sa > 0 && it.box.area() > 0.25 * sa && big.size() < 4 ? big : prims).push_back(it);
+    if (prims.size() < 2) {
+      prims = all;
+      big.clear();
+    }
+  }
   struct BN {
     Box box;
     int left = -1, right = -1;  // children (inner), or -1
@@ -1080,37 +1096,41 @@ bool Compiler::wide_bvh(const std::vector<Item>& prims, CompiledScene* out) {
     std::memcpy(&f, &u, 4);
     return f;
   };
+  auto put_prim = [&](uint32_t e) {  // the record of one primitive (rt_scene.h WNode)
+    const uint32_t ix = epay(e);
+    if (etype(e) == E_SPHERE) {
+      const Sphere<double>& s = spheres_[ix];
+      kinds |= WK_SPHERE | (s.moving ? WK_MOVING : 0u);
+      words.push_back({(float)s.c1[0], (float)s.c1[1], (float)s.c1[2], bits(e)});
+      words.push_back({(float)s.dc[0], (float)s.dc[1], (float)s.dc[2], (float)s.r});
+    } else if (etype(e) == E_TRI) {
+      const Tri<double>& t = tris_[ix];
+      kinds |= WK_TRI;
+      words.push_back({(float)t.p0[0], (float)t.p0[1], (float)t.p0[2], bits(e)});
+      words.push_back({(float)t.e1[0], (float)t.e1[1], (float)t.e1[2], 0.f});
+      words.push_back({(float)t.e2[0], (float)t.e2[1], (float)t.e2[2], 0.f});
+    } else if (etype(e) == E_QUAD) {
+      const Quad<double>& q = quads_[ix];
+      kinds |= WK_QUAD;
+      words.push_back({(float)q.q[0], (float)q.q[1], (float)q.q[2], bits(e)});
+      words.push_back({(float)q.n[0], (float)q.n[1], (float)q.n[2], (float)q.D});
+      words.push_back({(float)q.a[0], (float)q.a[1], (float)q.a[2], 0.f});
+      words.push_back({(float)q.b[0], (float)q.b[1], (float)q.b[2], 0.f});
+    } else {
+      return false;
+    }
+    return true;
+  };
+  for (const Item& it : big)
+    if (!put_prim(it.entry)) return false;
   auto leaf_code = [&](const BN& nd, uint32_t& code) {
     const size_t first = words.size();
     if (nd.count == 0 || nd.count > 64 || first > kWFirstMask) return false;
-    for (size_t i = nd.first; i < nd.first + nd.count; i++) {
-      const uint32_t e = prims[order[i]].entry, ix = epay(e);
-      if (etype(e) == E_SPHERE) {
-        const Sphere<double>& s = spheres_[ix];
-        kinds |= WK_SPHERE | (s.moving ? WK_MOVING : 0u);
-        words.push_back({(float)s.c1[0], (float)s.c1[1], (float)s.c1[2], bits(e)});
-        words.push_back({(float)s.dc[0], (float)s.dc[1], (float)s.dc[2], (float)s.r});
-      } else if (etype(e) == E_TRI) {
-        const Tri<double>& t = tris_[ix];
-        kinds |= WK_TRI;
-        words.push_back({(float)t.p0[0], (float)t.p0[1], (float)t.p0[2], bits(e)});
-        words.push_back({(float)t.e1[0], (float)t.e1[1], (float)t.e1[2], 0.f});
-        words.push_back({(float)t.e2[0], (float)t.e2[1], (float)t.e2[2], 0.f});
-      } else if (etype(e) == E_QUAD) {
-        const Quad<double>& q = quads_[ix];
-        kinds |= WK_QUAD;
-        words.push_back({(float)q.q[0], (float)q.q[1], (float)q.q[2], bits(e)});
-        words.push_back({(float)q.n[0], (float)q.n[1], (float)q.n[2], (float)q.D});
-        words.push_back({(float)q.a[0], (float)q.a[1], (float)q.a[2], 0.f});
-        words.push_back({(float)q.b[0], (float)q.b[1], (float)q.b[2], 0.f});
-      } else {
-        return false;
-      }
-    }
+    for (size_t i = nd.first; i < nd.first + nd.count; i++)
+      if (!put_prim(prims[order[i]].entry)) return false;
     code = kWLeaf | (uint32_t)(nd.count - 1) << kWCountShift | (uint32_t)first;
     return true;
   };
-
   std::vector<WNode> wn;
   // collapse: node of binary node `b` -> its index; stack need returned through `need`
   std::function<bool(int, uint32_t&, int&)> emit = [&](int b, uint32_t& code, int& need) -> bool {
@@ -1182,6 +1202,7 @@ bool Compiler::wide_bvh(const std::vector<Item>& prims, CompiledScene* out) {
   h.wroot = root;
   h.wide_stack = (uint32_t)std::max(1, need);
   h.wide_kinds = kinds;
+  h.wide_big = (uint32_t)big.size();
   h.has_wide = 1;
   return true;
 }

@@ -81,7 +81,8 @@ class rt_scene_info(ctypes.Structure):
     _fields_ = [("quads", c_int32), ("spheres", c_int32), ("triangles", c_int32), ("instances", c_int32),
                 ("volumes", c_int32), ("bvh_nodes", c_int32), ("linear_ops", c_int32), ("stack_need", c_int32),
                 ("bytes_f32", c_uint64), ("bytes_f64", c_uint64), ("flat_quads", c_int32), ("flat_boxes", c_int32),
-                ("wide_nodes", c_int32), ("wide_stack", c_int32), ("wide_kinds", c_int32), ("wide_prim_words", c_int32)]
+                ("wide_nodes", c_int32), ("wide_stack", c_int32), ("wide_kinds", c_int32), ("wide_prim_words", c_int32),
+                ("wide_big", c_int32)]
 
 
 # every symbol include/rt_hip.h declares, with its ctypes signature

@@ -238,6 +238,7 @@ typedef struct rt_scene_info {
   int32_t wide_stack; /*   stack entries a ray can need in it */
   int32_t wide_kinds; /*   primitive kinds present: 1 sphere, 2 triangle, 4 quad, 8 moving sphere */
   int32_t wide_prim_words; /* 16-byte words of its primitive records */
+  int32_t wide_big;        /*   primitives with scene-sized boxes, tested before its tree (e.g. a ground sphere) */
 } rt_scene_info;
 
 typedef struct rt_context rt_context;
