@@ -564,8 +564,31 @@ __device__ bool volume_t(const DevScene<R>& sc, const Volume<R>& v, V<R> wo, V<R
   V<R> bo = wo, bd = wd;
   if (v.inst >= 0) chain_in(sc.insts[v.inst], bo, bd);
   R t1, t2;
-  if (!list_closest(sc, epay(v.boundary), bo, bd, time, -Num<R>::inf(), Num<R>::inf(), t1)) return false;
-  if (!list_closest(sc, epay(v.boundary), bo, bd, time, t1 + R(0.0001), Num<R>::inf(), t2)) return false;
+  bool boxed = false;
+  if constexpr (sizeof(R) == 4) {
+    if (v.is_box) {
+      // box() boundary (fp32): the closest face hit over (-inf, inf) is the slab entry, the next one
+      // past it + 1e-4 the exit (volumne.h:21-22); the same t = (plane - o) * rcp(d) as the quad tests
+      const V<R> inv = rcp3(bd);
+      R tn = -Num<R>::inf(), tf = Num<R>::inf();
+      const R los[3] = {v.lo[0], v.lo[1], v.lo[2]}, his[3] = {v.hi[0], v.hi[1], v.hi[2]};
+      const R os[3] = {bo.x, bo.y, bo.z}, ds[3] = {bd.x, bd.y, bd.z}, is[3] = {inv.x, inv.y, inv.z};
+#pragma unroll
+      for (int a = 0; a < 3; a++) {
+        const R ta = fdiv_inv(los[a] - os[a], ds[a], is[a]), tb = fdiv_inv(his[a] - os[a], ds[a], is[a]);
+        tn = fmaxf(tn, fminf(ta, tb));
+        tf = fminf(tf, fmaxf(ta, tb));
+      }
+      if (!(tn <= tf) || !(tf >= tn + R(0.0001))) return false;
+      t1 = tn;
+      t2 = tf;
+      boxed = true;
+    }
+  }
+  if (!boxed) {
+    if (!list_closest(sc, epay(v.boundary), bo, bd, time, -Num<R>::inf(), Num<R>::inf(), t1)) return false;
+    if (!list_closest(sc, epay(v.boundary), bo, bd, time, t1 + R(0.0001), Num<R>::inf(), t2)) return false;
+  }
   if (t1 < tmin) t1 = tmin;
   if (t2 > tmax) t2 = tmax;
   if (t1 >= t2) return false;

@@ -160,12 +160,18 @@ struct alignas(16) Instance {
 
 // volumne.h:9-46: boundary = refs list at `boundary` (object space of chain `inst`,
 // -1 = world). neg_inv_density = -1.0 / density (volumne.h:36).
+// is_box: the boundary is the six quads of box() (quad.h:91-112) -- [lo, hi] in boundary space --
+// and the fp32 kernels find its entry and exit with one slab test instead of twelve quad tests.
 template <class R>
 struct alignas(16) Volume {
   R neg_inv_density;
   int32_t inst;
   uint32_t boundary;  // LIST entry of the boundary primitives
   int32_t phase_mat;
+  R lo[3];
+  int32_t is_box;
+  R hi[3];
+  int32_t pad;
 };
 
 template <class R>

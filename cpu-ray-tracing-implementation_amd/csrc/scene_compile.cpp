@@ -197,6 +197,7 @@ class Compiler {
   bool flat_program(const std::vector<uint32_t>& lin, std::vector<FlatQuad>& quads, uint32_t nq[3],
                     std::vector<FlatBox>& boxes);
   bool wide_bvh(const std::vector<Item>& prims, CompiledScene* out);
+  bool box_of_quads(const std::vector<Item>& prims, double lo[3], double hi[3]) const;
   std::vector<int> aligned_;  // per quad: 1 + perm for axis-aligned quads, 0 otherwise
   std::vector<double> qu_, qv_;  // per quad: u[U], v[V] (aligned quads)
   void light_from(int idx);
@@ -545,6 +546,7 @@ void Compiler::gather(int idx, const std::vector<Op>& chain, std::vector<Item>& 
       }
       Item bl = list_of(prims);
       Volume<double> v{};
+      v.is_box = box_of_quads(prims, v.lo, v.hi) ? 1 : 0;
       v.neg_inv_density = -1.0 / o->s0;
       v.inst = chain2.empty() ? -1 : make_instance(chain2, bl.entry);
       v.boundary = bl.entry;
@@ -671,7 +673,8 @@ Instance<float> to32(const Instance<double>& in) {
   return r;
 }
 Volume<float> to32(const Volume<double>& v) {
-  return {(float)v.neg_inv_density, v.inst, v.boundary, v.phase_mat};
+  return {(float)v.neg_inv_density, v.inst, v.boundary, v.phase_mat, {(float)v.lo[0], (float)v.lo[1], (float)v.lo[2]},
+          v.is_box, {(float)v.hi[0], (float)v.hi[1], (float)v.hi[2]}, 0};
 }
 Node<float> to32(const Node<double>& n) {
   Node<float> r{};
@@ -967,6 +970,35 @@ bool Compiler::flat_program(const std::vector<uint32_t>& lin, std::vector<FlatQu
     quads.insert(quads.end(), grp[a].begin(), grp[a].end());
   }
   return true;
+}
+
+// Six axis-aligned quads that are exactly the faces of one box (as box(), quad.h:91-112, makes them):
+// each axis has two face planes, and every face spans the box in its two in-plane axes.
+bool Compiler::box_of_quads(const std::vector<Item>& prims, double lo[3], double hi[3]) const {
+  if (prims.size() != 6) return false;
+  int cnt[3] = {0, 0, 0};
+  for (const Item& it : prims) {
+    if (etype(it.entry) != E_QUAD || !aligned_[epay(it.entry)]) return false;
+    const int A = kPermAxes[aligned_[epay(it.entry)] - 1][0];
+    const double plane = quads_[epay(it.entry)].q[A];
+    if (cnt[A] == 0) lo[A] = hi[A] = plane;
+    lo[A] = std::min(lo[A], plane);
+    hi[A] = std::max(hi[A], plane);
+    cnt[A]++;
+  }
+  for (int k = 0; k < 3; k++)
+    if (cnt[k] != 2 || !(lo[k] < hi[k])) return false;
+  int faces = 0;
+  for (const Item& it : prims) {
+    const uint32_t i = epay(it.entry);
+    const int* ax = kPermAxes[aligned_[i] - 1];  // A, axis of u, axis of v
+    const double q[3] = {quads_[i].q[0], quads_[i].q[1], quads_[i].q[2]};
+    const double u0 = std::min(q[ax[1]], q[ax[1]] + qu_[i]), u1 = std::max(q[ax[1]], q[ax[1]] + qu_[i]);
+    const double v0 = std::min(q[ax[2]], q[ax[2]] + qv_[i]), v1 = std::max(q[ax[2]], q[ax[2]] + qv_[i]);
+    if (u0 != lo[ax[1]] || u1 != hi[ax[1]] || v0 != lo[ax[2]] || v1 != hi[ax[2]]) return false;
+    faces |= 1 << (2 * ax[0] + (q[ax[0]] == hi[ax[0]] ? 1 : 0));
+  }
+  return faces == 63;
 }
 
 // The wide BVH of rt_scene.h (fp32 kernels) over world-level primitives: a binned SAH binary
