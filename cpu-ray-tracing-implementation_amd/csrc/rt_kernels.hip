@@ -60,8 +60,9 @@ constexpr int kBlock = 256;
 #ifndef RT_STACK_WAVES  // 4: the LDS limit of the LDS-node BVH kernel (32.8 KB per block); C3 151 -> 129 ms vs 3
 #define RT_STACK_WAVES 4
 #endif
-#ifndef RT_LINEAR_VOL_WAVES  // fp32 quad + volume linear program (C5): 1 (128 VGPRs, 4 waves) 3385 ms, 5: 4674, 6: 5933
-#define RT_LINEAR_VOL_WAVES 1
+#ifndef RT_LINEAR_VOL_WAVES  // fp32 quad + volume linear program (C5), with slab-tested box() volumes: 1 (4 waves at
+                             // 128 VGPRs) 1661 ms/frame, 5: 1567, 6: 2594 (spills)
+#define RT_LINEAR_VOL_WAVES 5
 #endif
 constexpr int kBatch = 16;           // extend/shade rounds between live-slot counts
 constexpr int kSegShards = 256;      // segment counter shards
