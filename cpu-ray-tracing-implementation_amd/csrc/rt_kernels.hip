@@ -54,6 +54,9 @@ constexpr int kBlock = 256;
 #ifndef RT_SPHERE_REFINE  // fp32 sphere hits: point and normal from an fp64 re-solve (shade)
 #define RT_SPHERE_REFINE 1
 #endif
+#ifndef RT_COLD_LDS  // the volume linear program: the cold path state in LDS (Path, LC)
+#define RT_COLD_LDS 1
+#endif
 #ifndef RT_PERSIST_MODE  // 2: dynamic (per-XCD heads), 1: static striding (development A/B)
 #define RT_PERSIST_MODE 2
 #endif
@@ -147,28 +150,90 @@ struct Params {
   uint32_t* fault;   // set when a lane hits seg_cap (internal error, reported by the host)
 };
 
-template <class R>
+// The per-lane words of the path state that only sample and item boundaries touch (LC paths,
+// below), in LDS as [word][lane]: 32-bit words, then the fp64 pixel base as [component][lane].
+constexpr int kColdWords = 8, kColdDoubles = 3;
+__device__ __forceinline__ uint32_t* cold_words() {
+  __shared__ uint32_t w[kColdWords * kBlock];
+  return w + threadIdx.x;
+}
+__device__ __forceinline__ double* cold_doubles() {
+  __shared__ double w[kColdDoubles * kBlock];
+  return w + threadIdx.x;
+}
+
+// One path's state. The fields a segment reads stay in registers; the cold ones -- the item's
+// running sum, its pixel and RNG key, the sample counter and range, the fp64 camera base -- are
+// registers too unless LC, where they live in the lane's LDS words (cold_words) so the trace and
+// shade code of the persistent loop gets their 14 VGPRs.
+template <class R, bool LC = false>
 struct Path {
-  V<R> o, d, thr, rad, acc;
+  V<R> o, d, thr, rad;
   R tm;
   int32_t bounce;
-  uint32_t ka, ks, item, sample;
+  uint32_t ks;
   uint32_t xe;
   int32_t xi;
-  uint32_t xy, send;
+  // cold state (register copies: unused when LC)
+  V<R> acc_;
+  uint32_t ka_, item_, sample_, send_, xy_;
 #if RT_CAM_BASE
-  V<double> cb;  // (dir00 + x du) + y dv of the item's pixel (pixel_base)
+  V<double> cb_;  // (dir00 + x du) + y dv of the item's pixel (pixel_base)
+#endif
+  enum { kAcc = 0, kKa = 3, kItem, kSample, kSend, kXy };
+  __device__ __forceinline__ static uint32_t& w(int k) { return cold_words()[k * kBlock]; }
+  __device__ __forceinline__ V<R> acc() const {
+    if constexpr (LC) return mkv(__uint_as_float(w(kAcc)), __uint_as_float(w(kAcc + 1)), __uint_as_float(w(kAcc + 2)));
+    else return acc_;
+  }
+  __device__ __forceinline__ void set_acc(V<R> v) {
+    if constexpr (LC) {
+      w(kAcc) = __float_as_uint(v.x);
+      w(kAcc + 1) = __float_as_uint(v.y);
+      w(kAcc + 2) = __float_as_uint(v.z);
+    } else {
+      acc_ = v;
+    }
+  }
+#define RT_COLD_U32(name, K)                                                        \
+  __device__ __forceinline__ uint32_t name() const {                                \
+    if constexpr (LC) return w(K); else return name##_;                             \
+  }                                                                                 \
+  __device__ __forceinline__ void set_##name(uint32_t v) {                          \
+    if constexpr (LC) w(K) = v; else name##_ = v;                                   \
+  }
+  RT_COLD_U32(ka, kKa)
+  RT_COLD_U32(item, kItem)
+  RT_COLD_U32(sample, kSample)
+  RT_COLD_U32(send, kSend)
+  RT_COLD_U32(xy, kXy)
+#undef RT_COLD_U32
+#if RT_CAM_BASE
+  __device__ __forceinline__ V<double> cb() const {
+    if constexpr (LC) return mkv(cold_doubles()[0], cold_doubles()[kBlock], cold_doubles()[2 * kBlock]);
+    else return cb_;
+  }
+  __device__ __forceinline__ void set_cb(V<double> v) {
+    if constexpr (LC) {
+      cold_doubles()[0] = v.x;
+      cold_doubles()[kBlock] = v.y;
+      cold_doubles()[2 * kBlock] = v.z;
+    } else {
+      cb_ = v;
+    }
+  }
 #endif
 };
+static_assert(Path<float>::kXy < kColdWords, "cold words");
 
 // The pixel's part of the perspective camera ray, (dir00 + x du) + y dv (camera.h:246-250): the
 // same for every sample of a work item, so it is computed once per item (and once per k_step
 // launch), not once per sample. Same operations in the same order: bit-identical.
-template <class R>
-__device__ __forceinline__ void pixel_base(const Params<R>& p, Path<R>& s) {
+template <class R, class PS>
+__device__ __forceinline__ void pixel_base(const Params<R>& p, PS& s, uint32_t xy) {
 #if RT_CAM_BASE
-  const double x = double(s.xy & 0xFFFFu), y = double(s.xy >> 16);
-  s.cb = (ld_here(&p.camx->dir00) + x * ld_here(&p.camx->du)) + y * ld_here(&p.camx->dv);
+  const double x = double(xy & 0xFFFFu), y = double(xy >> 16);
+  s.set_cb((ld_here(&p.camx->dir00) + x * ld_here(&p.camx->du)) + y * ld_here(&p.camx->dv));
 #endif
 }
 
@@ -183,16 +248,16 @@ __device__ __forceinline__ void load_path(const Params<R>& p, uint32_t slot, R4<
   s.bounce = (int32_t)Dv.w;
   s.thr = mkv(Tv.x, Tv.y, Tv.z);
   s.rad = mkv(Lv.x, Lv.y, Lv.z);
-  s.acc = mkv(Av.x, Av.y, Av.z);
-  s.ka = S.x;
+  s.set_acc(mkv(Av.x, Av.y, Av.z));
+  s.set_ka(S.x);
   s.ks = S.y;
-  s.item = S.z;
-  s.sample = S.w;
+  s.set_item(S.z);
+  s.set_sample(S.w);
   s.xe = X.x;
   s.xi = (int32_t)X.y;
-  s.xy = X.z;
-  s.send = X.w;
-  pixel_base(p, s);
+  s.set_xy(X.z);
+  s.set_send(X.w);
+  pixel_base(p, s, X.z);
 }
 
 template <class R>
@@ -202,9 +267,10 @@ __device__ __forceinline__ void store_path(const Params<R>& p, uint32_t slot, co
   p.O[slot] = {s.o.x, s.o.y, s.o.z, s.tm};
   p.T[slot] = {s.thr.x, s.thr.y, s.thr.z, R(0)};
   p.L[slot] = {s.rad.x, s.rad.y, s.rad.z, R(0)};
-  p.A[slot] = {s.acc.x, s.acc.y, s.acc.z, R(0)};
-  p.S[slot] = make_uint4(s.ka, s.ks, s.item, s.sample);
-  p.X[slot] = make_uint4(s.xe, (uint32_t)s.xi, s.xy, s.send);
+  const V<R> acc = s.acc();
+  p.A[slot] = {acc.x, acc.y, acc.z, R(0)};
+  p.S[slot] = make_uint4(s.ka(), s.ks, s.item(), s.sample());
+  p.X[slot] = make_uint4(s.xe, (uint32_t)s.xi, s.xy(), s.send());
 }
 
 // The wave's local queue [next, end) of the dynamic schedule, in LDS (two words per wave).
@@ -267,16 +333,17 @@ __device__ __forceinline__ uint32_t next_item_dyn(const Params<R>& p) {
 }
 
 // A new work item for the slot: its pixel and that pixel's RNG key.
-template <class R>
-__device__ __forceinline__ void begin_item(const Params<R>& p, Path<R>& s, uint32_t item) {
+template <class R, class PS>
+__device__ __forceinline__ void begin_item(const Params<R>& p, PS& s, uint32_t item) {
   const uint32_t chunk = (uint32_t)(((uint64_t)item * p.npix_m) >> p.npix_k);
   const uint32_t xy = p.pixmap[item - chunk * p.npix];
-  s.item = item;
-  s.sample = chunk * p.chunk;
-  s.send = min(s.sample + p.chunk, p.spp);
-  s.xy = xy;
-  s.ka = key_pixel(p.seed, (xy >> 16) * p.W + (xy & 0xFFFFu));
-  pixel_base(p, s);
+  const uint32_t first = chunk * p.chunk;
+  s.set_item(item);
+  s.set_sample(first);
+  s.set_send(min(first + p.chunk, p.spp));
+  s.set_xy(xy);
+  s.set_ka(key_pixel(p.seed, (xy >> 16) * p.W + (xy & 0xFFFFu)));
+  pixel_base(p, s, xy);
 }
 
 // camera::generate_ray for the orthonormal, fisheye and lens models (camera.h:252-290), reading
@@ -324,10 +391,9 @@ __device__ __forceinline__ void camera_ray(const CamDev* cp, uint32_t ks, uint32
 }
 
 // camera::generate_ray, perspective mode (camera.h:244-251,293): sample s.sample of the slot's pixel
-template <class R, bool CAMX>
-__device__ __forceinline__ void begin_sample(const Params<R>& p, Path<R>& s) {
-  s.ks = key_path(s.ka, key_sample(p.seed, p.first_sample + s.sample));
-  uint32_t x = s.xy & 0xFFFFu, y = s.xy >> 16;
+template <class R, bool CAMX, class PS>
+__device__ __forceinline__ void begin_sample(const Params<R>& p, PS& s) {
+  s.ks = key_path(s.ka(), key_sample(p.seed, p.first_sample + s.sample()));
   // In fp64 for both paths: fp32 gets the correctly rounded ray, a few ulp less error on every
   // camera ray, which otherwise shows up as paths crossing a checker line or edge differently.
   const double ox = to_unit<double>(draw_u32(s.ks, 0)) - 0.5;  // sample_square (camera.h:293)
@@ -337,13 +403,15 @@ __device__ __forceinline__ void begin_sample(const Params<R>& p, Path<R>& s) {
   if (!CAMX || p.cam_mode == RT_CAM_PERSPECTIVE) {  // camera.h:245-251
     const V<double> du = ld_here(&p.camx->du), dv = ld_here(&p.camx->dv);
 #if RT_CAM_BASE
-    d = (s.cb + ox * du) + oy * dv;
+    d = (s.cb() + ox * du) + oy * dv;
 #else
+    const uint32_t xy = s.xy(), x = xy & 0xFFFFu, y = xy >> 16;
     d = ((ld_here(&p.camx->dir00) + double(x) * du) + double(y) * dv + ox * du) + oy * dv;
 #endif
     tm = to_unit<double>(draw_u32(s.ks, 2));
   } else if constexpr (CAMX) {
-    camera_ray(p.camx, s.ks, x, y, ox, oy, o, d, tm);
+    const uint32_t xy = s.xy();
+    camera_ray(p.camx, s.ks, xy & 0xFFFFu, xy >> 16, ox, oy, o, d, tm);
   }
   s.o = mkv(R(o.x), R(o.y), R(o.z));
   s.d = mkv(R(d.x), R(d.y), R(d.z));
@@ -361,7 +429,7 @@ __global__ __launch_bounds__(kBlock) void k_init(Params<R> p) {
   uint32_t slot = blockIdx.x * kBlock + threadIdx.x;
   if (slot >= p.P) return;
   Path<R> s;
-  s.acc = mkv(R(0), R(0), R(0));
+  s.set_acc(mkv(R(0), R(0), R(0)));
   if (slot >= p.n_items) {
     s.d = mkv(R(0), R(0), R(0));
     s.bounce = -1;
@@ -378,8 +446,8 @@ __global__ __launch_bounds__(kBlock) void k_init(Params<R> p) {
 // has no work left.
 // FLAT: the hit comes from the flat program (trace_flat): a quad whose outward normal (+-e_A)
 // and material are packed in nm, so no primitive or instance record is read.
-template <class R, bool CAMX, bool FLAT = false>
-__device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t inst, uint32_t nm = 0) {
+template <class R, bool CAMX, bool FLAT = false, class PS>
+__device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, uint32_t nm = 0) {
   const DevScene<R>& sc = p.sc;
   V<R> add = mkv(R(0), R(0), R(0));
   bool has_add = false, done = false;
@@ -597,15 +665,19 @@ __device__ bool shade(const Params<R>& p, Path<R>& s, R t, uint32_t e, int32_t i
     return true;
   }
   // the sample is finished (camera.h:167): add it to the item's running sum
-  s.acc = s.acc + s.rad;
-  s.sample += 1;
-  if (s.sample >= s.send) {
-    R* dst = p.partial + 3ull * s.item;
-    dst[0] = s.acc.x;
-    dst[1] = s.acc.y;
-    dst[2] = s.acc.z;
-    s.acc = mkv(R(0), R(0), R(0));
-    const uint32_t nx = p.persist == 2 ? next_item_dyn(p) : (s.item + p.P < p.n_items ? s.item + p.P : kNoItem);
+  const V<R> acc = s.acc() + s.rad;
+  const uint32_t sample = s.sample() + 1;
+  s.set_sample(sample);
+  if (sample < s.send()) {
+    s.set_acc(acc);
+  } else {
+    const uint32_t item = s.item();
+    R* dst = p.partial + 3ull * item;
+    dst[0] = acc.x;
+    dst[1] = acc.y;
+    dst[2] = acc.z;
+    s.set_acc(mkv(R(0), R(0), R(0)));
+    const uint32_t nx = p.persist == 2 ? next_item_dyn(p) : (item + p.P < p.n_items ? item + p.P : kNoItem);
     if (nx == kNoItem) {
       s.bounce = -1;
       return false;
@@ -632,7 +704,10 @@ struct LinearTrav {
   static constexpr int kLdsNodes = 0;
   static constexpr bool kFlat = false;
   static constexpr bool kWide = false;
-  __device__ __forceinline__ static void run(const DevScene<R>& sc, const Node<R>*, const Path<R>& s, Keys k,
+  // the volume program's registers (C5: 23 -> 6 VGPRs spilled at 96, 1563 -> 1498 ms/frame)
+  static constexpr bool kColdLds = sizeof(R) == 4 && VOL && RT_COLD_LDS;
+  template <class PS>
+  __device__ __forceinline__ static void run(const DevScene<R>& sc, const Node<R>*, const PS& s, Keys k,
                                              uint32_t*, R& t, uint32_t& e, int32_t& i, uint32_t&) {
     trace_linear<R, SPH, TRI, VOL>(sc, s.o, s.d, s.tm, s.xe, s.xi, k, (uint32_t)s.bounce, t, e, i);
   }
@@ -647,7 +722,9 @@ struct FlatTrav {
   static constexpr int kLdsNodes = 0;
   static constexpr bool kFlat = true;
   static constexpr bool kWide = false;
-  __device__ __forceinline__ static void run(const DevScene<float>& sc, const Node<float>*, const Path<float>& s,
+  static constexpr bool kColdLds = false;  // 72 -> 64 VGPRs, but C2 23.5 -> 24.1 ms/frame
+  template <class PS>
+  __device__ __forceinline__ static void run(const DevScene<float>& sc, const Node<float>*, const PS& s,
                                              Keys, uint32_t*, float& t, uint32_t& e, int32_t& i, uint32_t& nm) {
     trace_flat(sc, s.o, s.d, s.xe, s.xi, t, e, i, nm);
   }
@@ -662,7 +739,9 @@ struct StackTrav {
   static constexpr int kWaves = sizeof(R) == 4 ? RT_STACK_WAVES : 1;  // fp32: occupancy over a small spill
   static constexpr bool kFlat = false;
   static constexpr bool kWide = false;
-  __device__ __forceinline__ static void run(const DevScene<R>& sc, const Node<R>* nodes, const Path<R>& s, Keys k,
+  static constexpr bool kColdLds = false;  // its LDS holds the traversal stacks
+  template <class PS>
+  __device__ __forceinline__ static void run(const DevScene<R>& sc, const Node<R>* nodes, const PS& s, Keys k,
                                              uint32_t* stk, R& t, uint32_t& e, int32_t& i, uint32_t&) {
     trace<R, STACK, kBlock>(sc, LDSN ? nodes : sc.nodes, s.o, s.d, s.tm, s.xe, s.xi, k, (uint32_t)s.bounce, stk,
                             t, e, i);
@@ -679,6 +758,9 @@ struct StackTrav {
 #ifndef RT_WIDE_WAVES_GLOBAL  // tree in HBM, 32-bit stack in LDS (C4 stand-in: 4 waves 519 ms, 5: 462)
 #define RT_WIDE_WAVES_GLOBAL 5
 #endif
+#ifndef RT_PARAM_RELOAD  // flat / linear / binary-BVH loops: parameters reloaded per segment
+#define RT_PARAM_RELOAD 1
+#endif
 #ifndef RT_SHADE_BATCH  // < 64: a wave stops traversing to shade once this many of its lanes have finished
 #define RT_SHADE_BATCH 64  // (measured on C3: 16 / 32 / 48 are 1-2 % slower than never pausing)
 #endif
@@ -689,6 +771,7 @@ struct WideTrav {
   static constexpr int kWaves = LDSN ? RT_WIDE_WAVES : RT_WIDE_WAVES_GLOBAL;
   static constexpr bool kFlat = false;
   static constexpr bool kWide = true;
+  static constexpr bool kColdLds = false;  // its LDS holds the tree and the stacks
   using StackT = WStackT<LDSN>;
   // LDS layout: [nodes, kWNodeLdsStride each][primitive words][stack: entries x kBlock of StackT]
   __host__ __device__ static uint32_t stack_offset(uint32_t n_wnodes, uint32_t n_words) {
@@ -714,7 +797,8 @@ struct WideTrav {
     return (StackT*)(base + stack_offset(sc.n_wnodes, sc.n_wprim_words));
   }
   // Advance the ray of s (false: paused, see trace_wide)
-  __device__ __forceinline__ static bool steps(const DevScene<float>& sc, const Node<float>* lds, const Path<float>& s,
+  template <class PS>
+  __device__ __forceinline__ static bool steps(const DevScene<float>& sc, const Node<float>* lds, const PS& s,
                                                StackT* stk, WideRay& ry) {
     const unsigned char* base = (const unsigned char*)lds;
     return trace_wide<SPH, TRI, QUAD, MOV, LDSN, kBlock, RT_SHADE_BATCH>(
@@ -836,8 +920,8 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
   }
   uint64_t segs = 0;
   if (item0 < p.n_items) {
-    Path<R> s;
-    s.acc = mkv(R(0), R(0), R(0));
+    Path<R, Trav::kColdLds> s;
+    s.set_acc(mkv(R(0), R(0), R(0)));
     begin_item(p, s, item0);
     begin_sample<R, CAMX>(p, s);
     if constexpr (Trav::kWide) {
@@ -847,28 +931,44 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
       WideRay ry{root, 0, Num<float>::inf(), kNoHit, 1u};
 #pragma unroll 1
       for (;;) {
-        if (!Trav::steps(p.sc, trav_nodes, s, (StackT*)wstk, ry)) continue;
-        if (++segs > p.seg_cap) {  // cannot happen: every segment advances a bounce-capped path
-          atomicOr(p.fault, 1u);
+        const Params<R>& q = p;  // (reloading q per segment as below: C3 1.5 % slower)
+        if (!Trav::steps(q.sc, trav_nodes, s, (StackT*)wstk, ry)) continue;
+        if (++segs > q.seg_cap) {  // cannot happen: every segment advances a bounce-capped path
+          atomicOr(q.fault, 1u);
           break;
         }
         const float t = ry.tmax;
         const uint32_t e = ry.e;
         ry = WideRay{root, 0, Num<float>::inf(), kNoHit, 1u};
-        if (!shade<R, CAMX, false>(p, s, t, e, -1, 0)) break;
+        if (!shade<R, CAMX, false>(q, s, t, e, -1, 0)) break;
       }
     } else {
+#if RT_PARAM_RELOAD
+      // The parameters are read from the kernarg segment afresh each segment (the asm hides
+      // the pointer from loop-invariant hoisting): hoisted, they outgrow the SGPR file and spill
+      // into VGPR lanes, one v_readlane per use (C2 flat program: 73 SGPR spills -> 0, 24.9 ->
+      // 23.9 ms/frame; scalar loads hit the constant cache)
+      using KP = const __attribute__((address_space(4))) Params<R>*;
+      const KP kp0 = (KP)__builtin_amdgcn_kernarg_segment_ptr();
+#endif
 #pragma unroll 1
       for (;;) {
+#if RT_PARAM_RELOAD
+        KP kp = kp0;
+        asm volatile("" : "+s"(kp));
+        const Params<R>& q = *(const Params<R>*)kp;
+#else
+        const Params<R>& q = p;
+#endif
         R t;
         uint32_t e, nm = 0;
         int32_t inst;
-        Trav::run(p.sc, trav_nodes, s, Keys{s.ks}, stk_lane, t, e, inst, nm);
-        if (++segs > p.seg_cap) {  // cannot happen: every segment advances a bounce-capped path
-          atomicOr(p.fault, 1u);
+        Trav::run(q.sc, trav_nodes, s, Keys{s.ks}, stk_lane, t, e, inst, nm);
+        if (++segs > q.seg_cap) {  // cannot happen: every segment advances a bounce-capped path
+          atomicOr(q.fault, 1u);
           break;
         }
-        if (!shade<R, CAMX, Trav::kFlat>(p, s, t, e, inst, nm)) break;
+        if (!shade<R, CAMX, Trav::kFlat>(q, s, t, e, inst, nm)) break;
       }
     }
   }
@@ -1387,8 +1487,12 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
                        (R*)dout, (uint64_t)out_elems);
   } else {
     const uint32_t spp = (uint32_t)prm->spp;
+    // the flat program's items are cheaper per sample, so its default items are twice as long
+    // (fewer item ends, dequeues and partial-sum stores; C2: 23.9 -> 23.5 ms/frame)
+    const bool flat_prog = !f64 && hdr.has_flat && prm->traversal != RT_TRAV_ORDERED &&
+                           make_view(cam).mode == RT_CAM_PERSPECTIVE && !(hdr.n_texdata > 0 || hdr.has_cell_noise);
     const uint32_t chunk = prm->samples_per_item > 0 ? std::min<uint32_t>((uint32_t)prm->samples_per_item, spp)
-                                                     : std::min<uint32_t>(kAutoChunk, spp);
+                                                     : std::min<uint32_t>(flat_prog ? 2 * kAutoChunk : kAutoChunk, spp);
     const uint32_t nchunks = (spp + chunk - 1) / chunk;
     const uint64_t n_items64 = (uint64_t)npix * nchunks;
     if (n_items64 >= (1ull << 31)) return set_err(c, RT_ERR_INVALID_ARGUMENT, "too many work items in one call");
