@@ -275,6 +275,17 @@ __device__ __forceinline__ void chain_in(const Instance<R>& in, V<R>& o, V<R>& d
     d = op_in(in.op[k], d, false);
   }
 }
+// the same for an instance held in registers (a scalar-loaded record): unrolled, so the ops
+// are indexed statically and the record is not copied to the stack
+template <class R>
+__device__ __forceinline__ void chain_in_regs(const Instance<R>& in, V<R>& o, V<R>& d) {
+#pragma unroll
+  for (int k = 0; k < kMaxChain; k++) {
+    if (k >= in.nops) break;
+    o = op_in(in.op[k], o, true);
+    d = op_in(in.op[k], d, false);
+  }
+}
 
 // ------------------------------------------------------------------ primitive tests
 // 1/d for the slab test: v_rcp_f32 in fp32 (its error is covered by box_slack), IEEE in fp64.
@@ -558,11 +569,20 @@ __device__ bool list_closest(const DevScene<R>& sc, uint32_t pos, V<R> o, V<R> d
 // volumne::hit (volumne.h:18-46). o, d: the ray as the volume sees it.
 // wo, wd: the world ray (the boundary's wrapper chain is absolute, world -> boundary space);
 // d: the ray as the volume itself sees it (its length scales the free-flight distance).
-template <class R>
+// UNI: the volume is the same for the whole wave (the linear program): v is already in SGPRs and
+// its instance is scalar-loaded too (a vector load of a uniform address costs a VMEM round trip).
+template <class R, bool UNI = false>
 __device__ bool volume_t(const DevScene<R>& sc, const Volume<R>& v, V<R> wo, V<R> wd, V<R> d, R time, R tmin,
                          R tmax, Keys k, uint32_t bounce, uint32_t& jv, R& t) {
   V<R> bo = wo, bd = wd;
-  if (v.inst >= 0) chain_in(sc.insts[v.inst], bo, bd);
+  if (v.inst >= 0) {
+    if constexpr (UNI) {
+      const Instance<R> in = ld_uniform(sc.insts, (uint32_t)v.inst);
+      chain_in_regs(in, bo, bd);
+    } else {
+      chain_in(sc.insts[v.inst], bo, bd);
+    }
+  }
   R t1, t2;
   bool boxed = false;
   if constexpr (sizeof(R) == 4) {
@@ -974,7 +994,8 @@ __device__ __forceinline__ void trace_linear(const DevScene<R>& sc, V<R> wo, V<R
       }
       inv = rcp3(d);
     } else if (VOL && ty == E_VOLUME) {
-      h = volume_t(sc, sc.vols[idx], wo, wd, d, time, tmin, tmax, keys, bounce, jv, th);
+      const Volume<R> vol = ld_uniform(sc.vols, idx);
+      h = volume_t<R, true>(sc, vol, wo, wd, d, time, tmin, tmax, keys, bounce, jv, th);
     } else {  // kInstEnd
       cur = -1;
       o = wo;

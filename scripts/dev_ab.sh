@@ -7,11 +7,6 @@ run() {  # name, env, args
   env $e timeout -k 10 200 python3 bench.py --no-cpu-baseline --f64-steps 0 "$@" > gpurun_out/ab/$v.json 2>gpurun_out/ab/$v.err
   python3 -c "import json;d=json.load(open('gpurun_out/ab/$v.json'));print('$v',d['ms_per_step'])"
 }
-run c2 "" --config c2
-run c2_nocold "RT_HIP_LIB=$B/librt_hip_nocold.so" --config c2
 run c5 "" --config c5 --steps 2 --warmup 1
-run c5_nocold "RT_HIP_LIB=$B/librt_hip_nocold.so" --config c5 --steps 2 --warmup 1
-run c5_vol6 "RT_HIP_LIB=$B/librt_hip_vol6.so" --config c5 --steps 2 --warmup 1
-run c5_vol4 "RT_HIP_LIB=$B/librt_hip_vol4.so" --config c5 --steps 2 --warmup 1
-run c1 "" --config c1
-run c1_nocold "RT_HIP_LIB=$B/librt_hip_nocold.so" --config c1
+run c5_prev "RT_HIP_LIB=$B/librt_hip_prev.so" --config c5 --steps 2 --warmup 1
+run c5b "" --config c5 --steps 2 --warmup 1
