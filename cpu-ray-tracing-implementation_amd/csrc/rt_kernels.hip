@@ -522,13 +522,15 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
           // not land near the fp32 root (a grazing double root) keeps it.
           const double cx = (double)sp.c1[0] + (double)s.tm * sp.dc[0], cy = (double)sp.c1[1] + (double)s.tm * sp.dc[1],
                        cz = (double)sp.c1[2] + (double)s.tm * sp.dc[2];
-          const double ox = oo.x, oy = oo.y, oz = oo.z, dx = dd.x, dy = dd.y, dz = dd.z;
-          const double fx = ox - cx, fy = oy - cy, fz = oz - cz, rr = sp.r;
-          const double a = dx * dx + dy * dy + dz * dz, b = dx * fx + dy * fy + dz * fz;
-          const double c = (fx * fx + fy * fy + fz * fz) - rr * rr, t0 = t;
-          const double at = a * t0 + b;
-          double td = t0 - ((at + b) * t0 + c) / (2.0 * at);
-          if (!(fabs(td - t0) <= 1e-4 * fabs(t0))) td = t0;
+          // g(t0) = |o + t0 d - c|^2 - r^2 needs fp64 (it cancels); the step g / g' is tiny next
+          // to t0, so g' = 2 d.(o + t0 d - c) and the quotient are fp32
+          const double ox = oo.x, oy = oo.y, oz = oo.z, dx = dd.x, dy = dd.y, dz = dd.z, t0 = t, rr = sp.r;
+          const double qx = (ox + t0 * dx) - cx, qy = (oy + t0 * dy) - cy, qz = (oz + t0 * dz) - cz;
+          const double g = (qx * qx + qy * qy + qz * qz) - rr * rr;
+          const float gp = 2.0f * ((float)qx * dd.x + (float)qy * dd.y + (float)qz * dd.z);
+          float step = fdiv((float)g, gp);
+          if (!(fabsf(step) <= 1e-4f * fabsf(t))) step = 0.0f;
+          const double td = t0 - (double)step;
           const double px = ox + td * dx, py = oy + td * dy, pz = oz + td * dz;
           po = mkv((float)px, (float)py, (float)pz);
           outward = mkv((float)(px - sp.cn[0]), (float)(py - sp.cn[1]), (float)(pz - sp.cn[2])) * fdiv(R(1), sp.r);

@@ -7,6 +7,7 @@ run() {  # name, env, args
   env $e timeout -k 10 200 python3 bench.py --no-cpu-baseline --f64-steps 0 "$@" > gpurun_out/ab/$v.json 2>gpurun_out/ab/$v.err
   python3 -c "import json;d=json.load(open('gpurun_out/ab/$v.json'));print('$v',d['ms_per_step'])"
 }
-run c5 "" --config c5 --steps 2 --warmup 1
-run c5_prev "RT_HIP_LIB=$B/librt_hip_prev.so" --config c5 --steps 2 --warmup 1
-run c5b "" --config c5 --steps 2 --warmup 1
+run c3 "" --config c3
+run c3_prev "RT_HIP_LIB=$B/librt_hip_prev.so" --config c3
+run c3b "" --config c3
+run c3_prevb "RT_HIP_LIB=$B/librt_hip_prev.so" --config c3
