@@ -1502,4 +1502,75 @@ void orc_kat_refract(const double v[3], const double n[3], double eta, double ou
 
 double orc_kat_reflectance(double cosine, double ri) { return omat::reflectance(cosine, ri); }
 
+int orc_kat_aabb_hit(const double a[3], const double b[3], const double o[3], const double d[3], double tmin,
+                     double tmax) {
+  return box3::points(v3_from(a), v3_from(b)).hit({v3_from(o), v3_from(d), 0}, ivl(tmin, tmax)) ? 1 : 0;
+}
+
+// closest hit over n spheres (xyzr[4k..4k+3]) through hittable_list (bvh = 0) or bvh_node (bvh = 1)
+int orc_kat_world_hit(const double* xyzr, int n, int bvh, const double o[3], const double d[3], double tmin,
+                      double tmax, double out[7]) {
+  std::vector<std::unique_ptr<osphere>> sp;
+  olist list;
+  for (int k = 0; k < n; k++) {
+    sp.emplace_back(osphere::make_static({xyzr[4 * k], xyzr[4 * k + 1], xyzr[4 * k + 2]}, xyzr[4 * k + 3], nullptr));
+    list.add(sp.back().get());
+  }
+  std::vector<std::unique_ptr<obvh>> pool;
+  std::vector<const ohit*> objs = list.objs;
+  const ohit* world = bvh ? obvh::build(objs, 0, objs.size(), pool) : static_cast<const ohit*>(&list);
+  hrec rec;
+  rngctx g;
+  if (!world->hit({v3_from(o), v3_from(d), 0}, ivl(tmin, tmax), rec, g)) return 0;
+  double r[7] = {rec.t, rec.p.x, rec.p.y, rec.p.z, rec.n.x, rec.n.y, rec.n.z};
+  std::memcpy(out, r, sizeof r);
+  return 1;
+}
+
+double orc_kat_sphere_pdf(const double c[3], double r, const double o[3], const double dir[3]) {
+  std::unique_ptr<osphere> s(osphere::make_static(v3_from(c), r, nullptr));
+  rngctx g;
+  return s->pdf_value(v3_from(o), v3_from(dir), g);
+}
+
+double orc_kat_cosine_pdf(const double n[3], const double dir[3]) {
+  pdfsel p;
+  make_onb(v3_from(n), p.onb_x, p.onb_y, p.onb_z);
+  return pdf_value(p, v3_from(dir));
+}
+
+// noise.h evaluated on given tables: kind 0 perlin (table = 256 offsets xyz, then perm_x, perm_y,
+// perm_z as the host draws them; turb(7) into out_turb), 1 value noise (resolution^3 values),
+// 2 worley, 3 voronoi (no table)
+void orc_kat_noise(int kind, const double* table, int resolution, const double* pts, int n, double* out,
+                   double* out_turb) {
+  onoise nz;
+  if (kind == 0) {
+    for (int i = 0; i < 256; i++) nz.rand_offset.emplace_back(table[3 * i], table[3 * i + 1], table[3 * i + 2]);
+    for (int i = 0; i < 256; i++) nz.perm_x.push_back((int)table[768 + i]);
+  } else if (kind == 1) {
+    nz.resolution = resolution;
+    for (int i = 0; i < resolution * resolution * resolution; i++) nz.values.push_back((float)table[i]);
+  }
+  for (int i = 0; i < n; i++) {
+    const v3 p(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]);
+    out[i] = kind == 0 ? nz.perlin(p) : kind == 1 ? nz.value(p) : onoise::cells(p, kind == 3);
+    if (kind == 0 && out_turb) out_turb[i] = nz.turb(7, p);
+  }
+}
+
+// kind 0: random_in_unit_sphere, 1: random_unit_vec, 2: random_cosine_direction, n vectors after
+// srand(seed), in the glibc-compat mode (the reference's rand() draws)
+void orc_kat_compat_draws(unsigned seed, int kind, int n, double* out) {
+  std::srand(seed);
+  rngctx g;
+  g.mode = ORC_RNG_COMPAT;
+  for (int i = 0; i < n; i++) {
+    const v3 v = kind == 0 ? random_on_sphere(g) : kind == 1 ? random_unit_vec(g) : random_cosine_direction(g);
+    out[3 * i] = v.x;
+    out[3 * i + 1] = v.y;
+    out[3 * i + 2] = v.z;
+  }
+}
+
 }  // extern "C"

@@ -81,6 +81,15 @@ int orc_kat_triangle_hit(const double p0[3], const double p1[3], const double p2
 void orc_kat_onb(const double n[3], double out[9]); /* x, y, z */
 void orc_kat_refract(const double v[3], const double n[3], double eta, double out[3]);
 double orc_kat_reflectance(double cosine, double ri);
+int orc_kat_aabb_hit(const double a[3], const double b[3], const double o[3], const double d[3], double tmin,
+                     double tmax);
+int orc_kat_world_hit(const double* xyzr, int n, int bvh, const double o[3], const double d[3], double tmin,
+                      double tmax, double out[7]); /* t, p, normal */
+double orc_kat_sphere_pdf(const double c[3], double r, const double o[3], const double dir[3]);
+double orc_kat_cosine_pdf(const double n[3], const double dir[3]);
+void orc_kat_compat_draws(unsigned seed, int kind, int n, double* out); /* 3n doubles */
+void orc_kat_noise(int kind, const double* table, int resolution, const double* pts, int n, double* out,
+                   double* out_turb);
 
 #ifdef __cplusplus
 }

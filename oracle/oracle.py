@@ -47,6 +47,14 @@ def lib():
         L.orc_kat_refract.argtypes = [D, D, dbl, D]
         L.orc_kat_reflectance.restype = dbl
         L.orc_kat_reflectance.argtypes = [dbl, dbl]
+        L.orc_kat_aabb_hit.argtypes = [D, D, D, D, dbl, dbl]
+        L.orc_kat_world_hit.argtypes = [D, i32, i32, D, D, dbl, dbl, D]
+        L.orc_kat_sphere_pdf.restype = dbl
+        L.orc_kat_sphere_pdf.argtypes = [D, dbl, D, D]
+        L.orc_kat_cosine_pdf.restype = dbl
+        L.orc_kat_cosine_pdf.argtypes = [D, D]
+        L.orc_kat_compat_draws.argtypes = [u32, i32, i32, D]
+        L.orc_kat_noise.argtypes = [i32, D, i32, D, i32, D, D]
         _lib = L
     return _lib
 
