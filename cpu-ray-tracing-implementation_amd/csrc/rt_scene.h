@@ -202,7 +202,8 @@ struct alignas(16) WNode {
 constexpr uint32_t kWLeaf = 0x80000000u;
 constexpr uint32_t kWCountShift = 25;  // leaf: up to 64 primitives, first word < 2^25
 constexpr uint32_t kWFirstMask = (1u << kWCountShift) - 1u;
-constexpr int kWLeafMax = 4;
+constexpr int kWLeafMax = 4;         // primitives per leaf (triangles, mixed kinds)
+constexpr int kWLeafMaxSpheres = 6;  // sphere-only trees (at most 8: the LDS code's 3-bit count)
 constexpr int kWideStackMax = 96;  // stack entries a ray may need in the wide tree (beyond LDS: a spill area)
 // primitive kinds present (SceneHeader::wide_kinds)
 enum : uint32_t { WK_SPHERE = 1u, WK_TRI = 2u, WK_QUAD = 4u, WK_MOVING = 8u };

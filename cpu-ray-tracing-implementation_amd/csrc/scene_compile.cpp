@@ -1035,6 +1035,14 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
     for (int k = 0; k < 3; k++) cen[3 * i + k] = prims[i].box.center(k);
   // binary build, iterative (meshes are deep); SAH with a node traversal cost of 1 primitive test
   constexpr int kBins = 32;
+  // leaves of up to kWLeafMax primitives, kWLeafMaxSpheres when all are spheres (a sphere test is
+  // cheap next to a node visit; C3: leaves of 1/2/3/4/5/6/7/8 spheres 82.8/69.2/71.9/66.3/64.9/
+  // 64.0/66.2/67.8 ms/frame; C4's triangles in HBM: 4 -> 742, 6 -> 817). A SAH leaf test on top
+  // (node cost 1-8 primitive tests) was no better than the fixed sizes.
+  bool all_spheres = true;
+  for (const Item& it : prims) all_spheres = all_spheres && etype(it.entry) == E_SPHERE;
+  size_t leaf_max = (size_t)(all_spheres ? kWLeafMaxSpheres : kWLeafMax);
+  if (const char* v = std::getenv("RT_DEV_WIDE_LEAF")) leaf_max = (size_t)std::max(1, std::min(8, std::atoi(v)));
   bn.push_back(BN{});
   bn[0].first = 0;
   bn[0].count = prims.size();
@@ -1049,7 +1057,7 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
       cb.grow(&cen[3 * order[i]]);
     }
     bn[(size_t)ni].box = bounds;
-    if (n <= (size_t)kWLeafMax) continue;  // a leaf: one 4-wide node's worth of tests
+    if (n <= leaf_max) continue;  // a leaf: one 4-wide node's worth of tests
     int axis = 0;
     for (int k = 1; k < 3; k++)
       if (cb.hi[k] - cb.lo[k] > cb.hi[axis] - cb.lo[axis]) axis = k;
