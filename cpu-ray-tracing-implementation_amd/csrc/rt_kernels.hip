@@ -754,14 +754,17 @@ struct StackTrav {
 // words -- is copied into the block's dynamic LDS at kernel start; the per-lane stack follows it
 // ([depth][lane], conflict-free). Otherwise nodes and primitives are read from global memory and
 // only the stack is in LDS. Dynamic LDS is sized from the compiled scene (wide_lds_bytes).
-#ifndef RT_WIDE_WAVES  // LDS-resident tree: 6 blocks of 26 KB per CU (C3: 4 waves 93.6 ms, 5: 86.2, 6: 83.0)
-#define RT_WIDE_WAVES 6
+#ifndef RT_WIDE_WAVES  // LDS-resident tree (C3: 4 waves 93.6 ms, 5: 86.2, 6: 83.0; with leaves of 6 spheres the
+#define RT_WIDE_WAVES 7  // block needs ~21 KB, so 7 fit a CU: 64.0 -> 62.2 despite 22 spilled VGPRs; 8: 67.8)
 #endif
 #ifndef RT_WIDE_WAVES_GLOBAL  // tree in HBM, 32-bit stack in LDS (C4 stand-in: 4 waves 519 ms, 5: 462)
 #define RT_WIDE_WAVES_GLOBAL 5
 #endif
 #ifndef RT_PARAM_RELOAD  // flat / linear / binary-BVH loops: parameters reloaded per segment
 #define RT_PARAM_RELOAD 1
+#endif
+#ifndef RT_WIDE_RELOAD
+#define RT_WIDE_RELOAD 0
 #endif
 #ifndef RT_SHADE_BATCH  // < 64: a wave stops traversing to shade once this many of its lanes have finished
 #define RT_SHADE_BATCH 64  // (measured on C3: 16 / 32 / 48 are 1-2 % slower than never pausing)
@@ -931,9 +934,19 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
       using StackT = typename Trav::StackT;
       const uint32_t root = Trav::root(p.sc);
       WideRay ry{root, 0, Num<float>::inf(), kNoHit, 1u};
+#if RT_WIDE_RELOAD
+      using KP = const __attribute__((address_space(4))) Params<R>*;
+      const KP kp0 = (KP)__builtin_amdgcn_kernarg_segment_ptr();
+#endif
 #pragma unroll 1
       for (;;) {
-        const Params<R>& q = p;  // (reloading q per segment as below: C3 1.5 % slower)
+#if RT_WIDE_RELOAD
+        KP kp = kp0;
+        asm volatile("" : "+s"(kp));
+        const Params<R>& q = *(const Params<R>*)kp;
+#else
+        const Params<R>& q = p;  // (reloading q per segment as below: C3 1.5 % slower at 6 waves)
+#endif
         if (!Trav::steps(q.sc, trav_nodes, s, (StackT*)wstk, ry)) continue;
         if (++segs > q.seg_cap) {  // cannot happen: every segment advances a bounce-capped path
           atomicOr(q.fault, 1u);
