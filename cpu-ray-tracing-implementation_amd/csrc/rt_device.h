@@ -583,7 +583,7 @@ __device__ bool volume_t(const DevScene<R>& sc, const Volume<R>& v, V<R> wo, V<R
       chain_in(sc.insts[v.inst], bo, bd);
     }
   }
-  R t1, t2;
+  R t1 = R(0), t2 = R(0);  // set by the slab test or by list_closest before any use
   bool boxed = false;
   if constexpr (sizeof(R) == 4) {
     if (v.is_box) {
