@@ -757,8 +757,9 @@ struct StackTrav {
 #ifndef RT_WIDE_WAVES  // LDS-resident tree (C3: 4 waves 93.6 ms, 5: 86.2, 6: 83.0; with leaves of 6 spheres the
 #define RT_WIDE_WAVES 7  // block needs ~21 KB, so 7 fit a CU: 64.0 -> 62.2 despite 22 spilled VGPRs; 8: 67.8)
 #endif
-#ifndef RT_WIDE_WAVES_GLOBAL  // tree in HBM, 32-bit stack in LDS (C4 stand-in: 4 waves 519 ms, 5: 462)
-#define RT_WIDE_WAVES_GLOBAL 5
+#ifndef RT_WIDE_WAVES_GLOBAL  // tree in HBM, 32-bit stack in LDS (C4 stand-in: 4 waves 519 ms, 5: 462; with the
+// speculative traversal 5: 424, 6: 412.5 -- 7 blocks of 24 KB stacks do not fit the 160 KB LDS)
+#define RT_WIDE_WAVES_GLOBAL 6
 #endif
 #ifndef RT_PARAM_RELOAD  // flat / linear / binary-BVH loops: parameters reloaded per segment
 #define RT_PARAM_RELOAD 1
