@@ -27,6 +27,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <tuple>
@@ -72,6 +73,33 @@ constexpr int kSegShards = 256;      // segment counter shards
 constexpr uint32_t kAutoPool32 = 1u << 21;
 constexpr uint32_t kAutoPool64 = 1u << 19;
 constexpr uint32_t kAutoChunk = 16;
+// The automatic item sizes (rt_render_params.samples_per_item = 0); RT_ITEM_* in the environment
+// override them for A/B runs (scripts/dev_tail.py)
+static uint32_t env_u32(const char* name, uint32_t dflt) {
+  const char* v = std::getenv(name);
+  return (v && *v) ? (uint32_t)std::strtoul(v, nullptr, 10) : dflt;
+}
+static double env_f64(const char* name, double dflt) {
+  const char* v = std::getenv(name);
+  return (v && *v) ? std::strtod(v, nullptr) : dflt;
+}
+// Bulk items: 8 samples (32 for the flat program, whose samples are cheap); at most
+// kMaxItemsPerPixel items per pixel in all (both sizes doubled until they fit), so a high-spp frame
+// (C5: 3840x2160 at 4096 spp) keeps its item count under 2^31 and its partial sums bounded.
+// Measured (ms/frame, full frame / one rank of eight, scripts/dev_tail.sh): C3 16 samples 62.5 /
+// 12.0, 8 with the last half in items of 4 61.2 / 8.9; C2 32 uniform 23.9 / 3.59, 32 with the last
+// eighth in items of 8 23.6 / 3.47, with the last quarter 23.7-23.9 / 3.38 (the one-GPU frame, the
+// headline, is kept).
+constexpr uint32_t kMaxItemsPerPixel = 256;
+static uint32_t auto_chunk(bool flat) {
+  return std::max(1u, flat ? env_u32("RT_ITEM_CHUNK_FLAT", 2 * kAutoChunk) : env_u32("RT_ITEM_CHUNK", kAutoChunk / 2));
+}
+static uint32_t auto_tail_chunk(bool flat) {
+  return std::max(1u, flat ? env_u32("RT_ITEM_TAIL_CHUNK_FLAT", 8) : env_u32("RT_ITEM_TAIL_CHUNK", 4));
+}
+static double auto_tail_frac(bool flat) {
+  return std::min(1.0, std::max(0.0, flat ? env_f64("RT_ITEM_TAIL_FRAC_FLAT", 0.125) : env_f64("RT_ITEM_TAIL_FRAC", 0.5)));
+}
 constexpr int kAutoSegments = 16;  // segments each slot advances per k_step launch
 // persistent schedule: upper bound of the grid's lanes. The dynamic schedule (persist 2) cuts the
 // grid to what the chip holds resident; the static one (persist 1) launches them all (~10x the
@@ -132,6 +160,9 @@ struct Params {
   const uint32_t* queue;   // live slots, or null = slots [0, n)
   uint32_t n;
   uint32_t P, npix, n_items, chunk, spp, first_sample, W;
+  // two item sizes: chunks [0, k_bulk) hold `chunk` samples, the later ones (the frame's last
+  // items in dequeue order) `tail_chunk` <= chunk samples each
+  uint32_t k_bulk, tail_chunk;
   uint64_t npix_m;  // item / npix = (item * npix_m) >> npix_k for every item < 2^31 (div_magic)
   uint32_t npix_k;
   int32_t max_depth;
@@ -337,10 +368,13 @@ template <class R, class PS>
 __device__ __forceinline__ void begin_item(const Params<R>& p, PS& s, uint32_t item) {
   const uint32_t chunk = (uint32_t)(((uint64_t)item * p.npix_m) >> p.npix_k);
   const uint32_t xy = p.pixmap[item - chunk * p.npix];
-  const uint32_t first = chunk * p.chunk;
+  // fp64 items are uniform (the host never gives them a tail): compiled out, the select costs
+  // the fp64 Cornell kernel 10 VGPRs, 3 -> 2 waves per SIMD (C2 f64 5.22 -> 4.08 Gsamples/s)
+  const bool bulk = sizeof(R) == 8 || chunk < p.k_bulk;
+  const uint32_t first = bulk ? chunk * p.chunk : p.k_bulk * p.chunk + (chunk - p.k_bulk) * p.tail_chunk;
   s.set_item(item);
   s.set_sample(first);
-  s.set_send(min(first + p.chunk, p.spp));
+  s.set_send(min(first + (bulk ? p.chunk : p.tail_chunk), p.spp));
   s.set_xy(xy);
   s.set_ka(key_pixel(p.seed, (xy >> 16) * p.W + (xy & 0xFFFFu)));
   pixel_base(p, s, xy);
@@ -1507,9 +1541,26 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     // (fewer item ends, dequeues and partial-sum stores; C2: 23.9 -> 23.5 ms/frame)
     const bool flat_prog = !f64 && hdr.has_flat && prm->traversal != RT_TRAV_ORDERED &&
                            make_view(cam).mode == RT_CAM_PERSPECTIVE && !(hdr.n_texdata > 0 || hdr.has_cell_noise);
-    const uint32_t chunk = prm->samples_per_item > 0 ? std::min<uint32_t>((uint32_t)prm->samples_per_item, spp)
-                                                     : std::min<uint32_t>(flat_prog ? 2 * kAutoChunk : kAutoChunk, spp);
-    const uint32_t nchunks = (spp + chunk - 1) / chunk;
+    const uint32_t chunk0 = prm->samples_per_item > 0 ? std::min<uint32_t>((uint32_t)prm->samples_per_item, spp)
+                                                     : std::min<uint32_t>(f64 ? kAutoChunk : auto_chunk(flat_prog), spp);
+    // The frame's last items are short (auto item size only): a lane that takes a long item just
+    // before the queue runs dry keeps its wave resident while the others idle, and a small frame
+    // (one rank of eight) has few items per lane. The last tail_samples of every pixel come in
+    // items of tail_chunk samples; both depend on spp alone, so the image is the same for any
+    // tiling or rank count.
+    uint32_t chunk = chunk0, tail_chunk = chunk0, k_bulk = (spp + chunk0 - 1) / chunk0, nchunks = k_bulk;
+    if (prm->samples_per_item <= 0 && !f64) {  // fp64: uniform items of 16 (C2 f64 with the fp32
+                                                // layout: 5.22 -> 4.04 Gsamples/s)
+      const uint32_t ts = std::min<uint32_t>(spp, (uint32_t)((double)spp * auto_tail_frac(flat_prog) + 0.5));
+      tail_chunk = std::min(chunk, auto_tail_chunk(flat_prog));
+      for (;;) {
+        k_bulk = (spp - ts) / chunk;  // bulk items cover [0, k_bulk * chunk)
+        nchunks = k_bulk + (spp - k_bulk * chunk + tail_chunk - 1) / tail_chunk;
+        if (nchunks <= kMaxItemsPerPixel || chunk >= spp) break;
+        chunk = std::min(spp, 2 * chunk);
+        tail_chunk = std::min(chunk, 2 * tail_chunk);
+      }
+    }
     const uint64_t n_items64 = (uint64_t)npix * nchunks;
     if (n_items64 >= (1ull << 31)) return set_err(c, RT_ERR_INVALID_ARGUMENT, "too many work items in one call");
     const uint32_t n_items = (uint32_t)n_items64;
@@ -1577,6 +1628,8 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     div_magic(npix, p.npix_m, p.npix_k);
     p.n_items = n_items;
     p.chunk = chunk;
+    p.k_bulk = k_bulk;
+    p.tail_chunk = tail_chunk;
     p.spp = spp;
     p.first_sample = (uint32_t)std::max(0, prm->first_sample);
     p.W = (uint32_t)cam->image_width;

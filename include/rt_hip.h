@@ -183,8 +183,11 @@ typedef struct rt_render_params {
   uint64_t seed;            /* counter-RNG key; pixel (x, y) sample s is keyed by (seed, y*W+x, s) */
   int32_t precision;        /* rt_precision */
   int32_t first_sample;     /* render samples [first_sample, first_sample + spp) of each pixel */
-  int32_t samples_per_item; /* samples one work item accumulates (0 = auto: min(spp, 16)). The per-pixel sum
-                               is grouped by item, so this changes the image only by rounding. */
+  int32_t samples_per_item; /* samples one work item accumulates. 0 = auto, from spp alone: items of 8
+                               samples (32 on the flat program), the last half (eighth) of each pixel's
+                               samples in items of 4 (8), at most 256 items per pixel; fp64: items of 16.
+                               The per-pixel sum is grouped by item, so this changes the image only by
+                               rounding. */
   int32_t pool_slots;       /* path slots: lanes of the persistent kernel, or the wavefront pool
                                (0 = auto). Does not change the image. */
   int32_t segments_per_launch; /* 0 = the persistent schedule (one launch, path state in registers);
