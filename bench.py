@@ -3,7 +3,7 @@
 
 Workload (BASELINE.json configs[1]): the reference's Cornell Box
 (main.cc:198-225) at 800x800, 1024 spp, max depth 50, light importance sampling on.
-One step = one full frame. The framebuffer is cut into 32x32 tiles dealt
+One step = one full frame. The framebuffer is cut into 16x16 tiles dealt
 round-robin to the ranks; each rank renders its tiles on its GPU and rank 0
 gathers them (RCCL, torch.distributed "nccl") into the full linear framebuffer.
 
@@ -314,7 +314,7 @@ def main():
             "data": asset or "synthetic (the reference's scene, procedurally built; no assets)",
             "config": {"workload": f"{scene_name} {W}x{H} {spp}spp depth {depth}, light sampling on",
                        "key": key, "src_sha": buildinfo.src_sha(),
-                       "image": [W, H], "spp": spp, "max_depth": depth, "tiles": "32x32 round-robin over ranks",
+                       "image": [W, H], "spp": spp, "max_depth": depth, "tiles": "16x16 round-robin over ranks",
                        "parallelism": f"tiles{world}", "segments_per_sample": round(seg_per_sample, 4),
                        "segments_total": segs_total / args.steps, "kernel_timing": args.kernel_timing,
                        "rounds_per_frame": iters // max(1, args.steps), "grid_lanes": st.grid_lanes},

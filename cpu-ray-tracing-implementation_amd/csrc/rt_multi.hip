@@ -166,7 +166,7 @@ extern "C" {
 int32_t rt_multi_plan(int32_t width, int32_t height, int32_t ndev, int32_t tile_size, int32_t rank,
                       rt_tile* tiles_out, int32_t cap) {
   if (width <= 0 || height <= 0 || ndev <= 0 || rank < 0 || rank >= ndev || cap < 0) return -1;
-  const int32_t ts = tile_size > 0 ? tile_size : 32;
+  const int32_t ts = tile_size > 0 ? tile_size : 16;
   const std::vector<rt_tile> t = plan_rank(width, height, ndev, ts, rank);
   if (tiles_out)
     for (int32_t i = 0; i < (int32_t)t.size() && i < cap; i++) tiles_out[i] = t[i];
@@ -270,7 +270,7 @@ rt_status rt_multi_render(rt_multi* m, const rt_camera_desc* cam, const rt_rende
     return merr(m, RT_ERR_INVALID_ARGUMENT, "unknown precision");
   const int32_t W = cam->image_width, H = cam->image_height, n = (int32_t)m->devs.size();
   if (W <= 0 || H <= 0) return merr(m, RT_ERR_INVALID_ARGUMENT, "empty image");
-  const int32_t ts = tile_size > 0 ? tile_size : 32;
+  const int32_t ts = tile_size > 0 ? tile_size : 16;
   const bool f64 = prm->precision == RT_PREC_F64;
   const size_t elem = f64 ? sizeof(double) : sizeof(float);
 

@@ -1,9 +1,9 @@
-"""Framebuffer partitioning across ranks: 32x32 tiles dealt
+"""Framebuffer partitioning across ranks: 16x16 tiles dealt
 round-robin, each rank renders its tiles packed in order, rank 0 gathers the
 equal-size padded buffers and scatters them into the full framebuffer."""
 import numpy as np
 
-TILE = 32
+TILE = 16
 
 
 def all_tiles(w, h, ts=TILE):

@@ -204,7 +204,7 @@ class camera {
   // non-empty: render on these devices, tiles of tile_size_ dealt round-robin and gathered over RCCL
   // to devices_[0] (rt_multi_*; replaces camera.h:154-172's per-row par_unseq)
   std::vector<int32_t> devices_;
-  int tile_size_ = 32;
+  int tile_size_ = 16;
   rt_precision precision_ = RT_PREC_F32;  // RT_PREC_F64: the fp64 parity path
   uint64_t seed_ = 1;                   // counter-RNG key
   std::string last_error_;

@@ -305,7 +305,7 @@ int32_t rt_multi_uses_rccl(const rt_multi* m);
 /* rt_scene_upload on every device. */
 rt_status rt_multi_scene_upload(rt_multi* m, const rt_scene_desc* desc);
 /* The whole image into out_rgb: host memory, W * H * 3 floats (RT_PREC_F32) or doubles (RT_PREC_F64),
- * row-major, top row first. tile_size <= 0 selects 32. */
+ * row-major, top row first. tile_size <= 0 selects 16. */
 rt_status rt_multi_render(rt_multi* m, const rt_camera_desc* cam, const rt_render_params* params,
                           int32_t tile_size, void* out_rgb);
 /* Counters of rank `rank` (0 <= rank < ndev) since rt_multi_create; aux_ms of rank 0 holds the

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--pool", type=int, default=0)
     ap.add_argument("--chunk", type=int, default=0)
+    ap.add_argument("--ts", type=int, default=32, help="tile edge (rt_amd.tiling.TILE = 32)")
     args = ap.parse_args()
     scene_name, width, aspect, spp, depth = CONFIGS[args.config]
     cs = plugin.ConfigScene(scene_name, width, aspect)
@@ -41,7 +42,7 @@ def main():
     params = ctx.params(spp, depth, 1, abi.RT_PREC_F32, samples_per_item=args.chunk, pool_slots=args.pool)
     base = None
     for world in [int(x) for x in args.worlds.split(",")]:
-        all_tiles, counts, maxpix = plan(W, H, world)
+        all_tiles, counts, maxpix = plan(W, H, world, ts=args.ts)
         out = torch.zeros((maxpix, 3), dtype=torch.float32, device=dev)
         per_rank, kern = [], []
         for r in range(world):
