@@ -19,7 +19,7 @@ import torch  # noqa: E402
 
 import rt_amd  # noqa: E402
 from rt_amd import abi, plugin  # noqa: E402
-from rt_amd.tiling import plan  # noqa: E402
+from rt_amd.tiling import TILE, plan  # noqa: E402
 from bench import CONFIGS  # noqa: E402
 
 
@@ -30,7 +30,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--pool", type=int, default=0)
     ap.add_argument("--chunk", type=int, default=0)
-    ap.add_argument("--ts", type=int, default=32, help="tile edge (rt_amd.tiling.TILE = 32)")
+    ap.add_argument("--ts", type=int, default=TILE, help="tile edge (default rt_amd.tiling.TILE)")
     args = ap.parse_args()
     scene_name, width, aspect, spp, depth = CONFIGS[args.config]
     cs = plugin.ConfigScene(scene_name, width, aspect)
