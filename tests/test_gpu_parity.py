@@ -454,3 +454,26 @@ def test_glass_fox_matches_oracle(ctx, monkeypatch):
     img32, _, _ = render_both(ctx, cs.desc, cs.cam, 8, 5, 3, F32)
     print("glass_fox fp32 rmse", rmse(img32, ref), "divergent px", int((np.abs(img32 - ref).max(-1) > 1e-3).sum()))
     assert (rmse(img32, ref) < 1e-3).all(), rmse(img32, ref)
+
+
+@pytest.mark.parametrize("name,spp", [("cornell_box", 64), ("rtow", 24)])
+def test_auto_item_layout_with_tail_is_tiling_invariant(ctx, name, spp):
+    # the automatic item layout (rt_hip.h samples_per_item = 0) has bulk items and, for each pixel's
+    # last samples, shorter tail items (cornell_box, flat program: 1 bulk item of 32 + 4 of 8; rtow:
+    # 1 of 8 + 4 of 4); it depends on spp alone, so a split render equals the full one bit for bit,
+    # and it only regroups each pixel's sum (equal to uniform items up to rounding)
+    desc, cam, _, _ = scenes.SCENES[name](width=48, aspect=1.0 if name == "cornell_box" else 1.5)
+    ctx.upload(desc)
+    base = ctx.render(cam, spp, 8, seed=5, precision=F32)
+    from rt_amd.tiling import pixel_index, plan
+    W, H = cam.image_width, cam.image_height
+    for world in (2, 3):
+        tiles, _, _ = plan(W, H, world, ts=16)
+        fb = np.zeros((H * W, 3), dtype=base.dtype)
+        for r in range(world):
+            fb[pixel_index(tiles[r], W)] = ctx.render(cam, spp, 8, seed=5, precision=F32, tiles=tiles[r])
+        assert np.array_equal(fb.reshape(base.shape), base), world
+    uniform = ctx.render(cam, spp, 8, seed=5, precision=F32, samples_per_item=spp)
+    np.testing.assert_allclose(uniform, base, rtol=1e-5, atol=1e-6)
+    ref, _ = oracle.render(oracle.from_desc(desc), cam, spp, 8, seed=5)
+    assert (rmse(base.astype(np.float64), ref) < 1e-3).all(), rmse(base.astype(np.float64), ref)
