@@ -1260,10 +1260,13 @@ rt_status set_err(rt_context* c, rt_status s, const std::string& m) {
       return set_err((ctx), RT_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
   } while (0)
 
+// Grow a context buffer. The only work that can still read the old buffer is this context's
+// outstanding device-output render (host-output renders return finished, and a render on another
+// stream waits for pend_stream first): wait for that stream, not for the whole device.
 rt_status ensure(rt_context* c, DevBuf& b, size_t bytes) {
   if (b.ptr && b.bytes >= bytes) return RT_OK;
   if (b.ptr) {
-    RT_HIP(c, hipDeviceSynchronize());
+    if (c->pending) RT_HIP(c, hipStreamSynchronize(c->pend_stream));
     RT_HIP(c, hipFree(b.ptr));
     b.ptr = nullptr;
     b.bytes = 0;
@@ -1510,6 +1513,10 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     const std::vector<unsigned char>& blob = f64 ? cs.blob64 : cs.blob32;
     RT_HIP(c, hipMemcpyAsync(sbase, blob.data(), blob.size(), hipMemcpyHostToDevice, st));
     dirty = false;
+    // outstanding from here on, whatever this call does next (an empty tile list or max_depth <= 0
+    // launches nothing that reads the scene): a later render on another stream waits for st
+    c->pending = true;
+    c->pend_stream = st;
   }
 
   // pixel map: tiles packed in order, row-major inside each tile (expanded by k_pixmap)
@@ -1792,6 +1799,9 @@ rt_status rt_context_create(int32_t device, rt_context** out) {
 void rt_context_destroy(rt_context* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
+  // an outstanding device-output render still reads the buffers freed below (its fault word is
+  // dropped with the context: nobody is left to report it to)
+  if (c->pending) (void)hipStreamSynchronize(c->pend_stream);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->scene32, &c->scene64, &c->state, &c->partial, &c->pixmap, &c->queue0, &c->queue1, &c->blk, &c->wide_spill,
                     &c->out_tmp, &c->counters, &c->camx, &c->heads, &c->tiles, &c->fault})
@@ -1875,9 +1885,11 @@ rt_status rt_render_tiles(rt_context* c, const rt_camera_desc* cam, const rt_ren
       return set_err(c, RT_ERR_INVALID_ARGUMENT, "tile " + std::to_string(t) + " outside the image");
   }
   RT_HIP(c, hipSetDevice(c->device));
-  // NULL is the HIP null stream (torch's default stream), so work the caller queues after this call
-  // on that stream -- a clone, a gather -- is ordered after the render
-  hipStream_t st = (hipStream_t)stream;
+  // Device output: NULL is the HIP null stream (torch's default stream), so work the caller queues
+  // after this call on that stream -- a clone, a gather -- is ordered after the render. Host output
+  // (the call returns the finished image): NULL is the context's own non-blocking stream, so contexts
+  // driven from different host threads do not serialise on the null stream.
+  hipStream_t st = (stream == nullptr && !out_is_device) ? c->stream : (hipStream_t)stream;
   try {
     if (prm->precision == RT_PREC_F64) return render<double>(c, cam, prm, tiles, ntiles, out_rgb, out_is_device, st);
     return render<float>(c, cam, prm, tiles, ntiles, out_rgb, out_is_device, st);
@@ -1899,10 +1911,10 @@ rt_status rt_stats(rt_context* c, rt_counters* out) {
 rt_status rt_reset_counters(rt_context* c) {
   if (!c) return set_err(nullptr, RT_ERR_INVALID_ARGUMENT, "null context");
   RT_HIP(c, hipSetDevice(c->device));
-  const rt_status s = settle(c);
-  RT_HIP(c, hipMemset(c->counters.ptr, 0, sizeof(unsigned long long) * kSegShards));
-  if (c->fault.ptr) RT_HIP(c, hipMemset(c->fault.ptr, 0, 4));
-  RT_HIP(c, hipDeviceSynchronize());
+  const rt_status s = settle(c);  // nothing of this context is outstanding after it
+  RT_HIP(c, hipMemsetAsync(c->counters.ptr, 0, sizeof(unsigned long long) * kSegShards, c->stream));
+  if (c->fault.ptr) RT_HIP(c, hipMemsetAsync(c->fault.ptr, 0, 4, c->stream));
+  RT_HIP(c, hipStreamSynchronize(c->stream));
   c->last = rt_counters{};
   return s;
 }

@@ -19,6 +19,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <mutex>
 #include <set>
@@ -81,6 +82,7 @@ const Rccl& rccl() {
 
 std::mutex g_multi_err_mu;
 std::string g_multi_create_err;
+std::atomic<uint64_t> g_comm_inits{0};  // ncclCommInitAll calls (rt_multi_comm_inits)
 
 }  // namespace
 
@@ -140,11 +142,15 @@ std::vector<rt_tile> plan_rank(int32_t W, int32_t H, int32_t n, int32_t ts, int3
   return out;
 }
 
+// Grow a buffer on device `dev`. rt_multi_render returns with every rank's stream drained, so only
+// the streams of this rt_multi on that device can still hold work touching it: wait for those, not
+// for the whole device (other contexts on it keep running).
 rt_status ensure_dev(rt_multi* m, int dev, void*& p, size_t& have, size_t want) {
   if (p && have >= want) return RT_OK;
   MHIP(m, hipSetDevice(dev));
   if (p) {
-    MHIP(m, hipDeviceSynchronize());
+    for (size_t r = 0; r < m->devs.size(); r++)
+      if (m->devs[r] == dev && m->streams[r]) MHIP(m, hipStreamSynchronize(m->streams[r]));
     MHIP(m, hipFree(p));
     p = nullptr;
     have = 0;
@@ -180,6 +186,8 @@ const char* rt_multi_last_error(const rt_multi* m) {
 }
 
 int32_t rt_multi_uses_rccl(const rt_multi* m) { return m && m->use_rccl ? 1 : 0; }
+
+uint64_t rt_multi_comm_inits(void) { return g_comm_inits.load(); }
 
 void rt_multi_destroy(rt_multi* m) {
   if (!m) return;
@@ -244,6 +252,7 @@ rt_status rt_multi_create(const int32_t* devices, int32_t ndev, rt_multi** out) 
     if (!R.ok) return fail(RT_ERR_UNSUPPORTED, R.err);
     m->comms.assign(ndev, nullptr);
     const ncclResult_t nr = R.init_all(m->comms.data(), ndev, m->devs.data());
+    g_comm_inits.fetch_add(1);
     if (nr != ncclSuccess) {
       m->comms.clear();
       return fail(RT_ERR_HIP, std::string("ncclCommInitAll: ") + R.error_string(nr));

@@ -26,7 +26,7 @@ RT_TEX_SOLID, RT_TEX_CHECKER, RT_TEX_PERLIN, RT_TEX_VALUE, RT_TEX_WORLEY, RT_TEX
 RT_CAM_PERSPECTIVE, RT_CAM_ORTHONORMAL, RT_CAM_FISHEYE, RT_CAM_LENS = range(4)
 RT_PREC_F32, RT_PREC_F64 = 0, 1
 RT_TRAV_AUTO, RT_TRAV_ORDERED = 0, 1
-ABI_VERSION = 6  # include/rt_hip.h RT_ABI_VERSION
+ABI_VERSION = 7  # include/rt_hip.h RT_ABI_VERSION
 
 
 class rt_object(ctypes.Structure):
@@ -109,6 +109,7 @@ SIGNATURES = {
                                   c_int32, ctypes.c_void_p]),
     "rt_multi_stats": (c_int32, [ctypes.c_void_p, c_int32, ctypes.POINTER(rt_counters)]),
     "rt_multi_plan": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int32, ctypes.POINTER(rt_tile), c_int32]),
+    "rt_multi_comm_inits": (c_uint64, []),
 }
 
 _lib = None

@@ -28,6 +28,11 @@ def load():
         L.rtsc_render_ppm_on.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ctypes.c_int32), ctypes.c_int,
                                          ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
+        L.rtsc_render_ppm_repeat.restype = ctypes.c_int
+        L.rtsc_render_ppm_repeat.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_uint64, ctypes.c_int,
+                                             ctypes.POINTER(ctypes.c_int32), ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
         L.rtsc_render_ppm.restype = ctypes.c_int
         L.rtsc_render_ppm.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_uint64, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
@@ -56,14 +61,16 @@ class ConfigScene:
             self._h = None
 
 
-def render_ppm(name, path, width=0, aspect=0.0, spp=0, max_depth=0, seed=1, precision=abi.RT_PREC_F32, devices=None):
+def render_ppm(name, path, width=0, aspect=0.0, spp=0, max_depth=0, seed=1, precision=abi.RT_PREC_F32, devices=None,
+               repeat=1):
     """camera::render(of, world, light) of a config scene into a PPM file (the whole drop-in path);
-    devices: camera::devices_ (the image tiled over those GPUs through rt_multi_*)."""
+    devices: camera::devices_ (the image tiled over those GPUs through rt_multi_*); repeat: render that
+    many times with the same camera object (it keeps its contexts / communicator between renders)."""
     err = ctypes.create_string_buffer(512)
     devs = list(devices or [])
     arr = (ctypes.c_int32 * max(1, len(devs)))(*devs)
-    rc = load().rtsc_render_ppm_on(name.encode(), width, aspect, spp, max_depth, seed, precision, arr, len(devs),
-                                   path.encode(), err, 512)
+    rc = load().rtsc_render_ppm_repeat(name.encode(), width, aspect, spp, max_depth, seed, precision, arr, len(devs),
+                                       repeat, path.encode(), err, 512)
     if rc != 0:
         raise RuntimeError(f"camera::render failed: {err.value.decode()}")
 

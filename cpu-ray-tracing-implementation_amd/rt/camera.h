@@ -117,29 +117,37 @@ class camera {
       out = px32.data();
     }
     if (!devices_.empty()) {  // the image tiled over several GPUs, one RCCL gather (rt_multi_*)
-      rt_multi* mg = nullptr;
-      if (rt_multi_create(devices_.data(), (int32_t)devices_.size(), &mg) != RT_OK)
-        return fail(rt_multi_last_error(nullptr));
-      rt_status s = rt_multi_scene_upload(mg, &desc);
-      if (s == RT_OK) s = rt_multi_render(mg, &cam, &p, tile_size_, out);
+      if (!multi_ || multi_devs_ != devices_) {  // kept across renders on the same devices
+        multi_.reset();
+        rt_multi* mg = nullptr;
+        if (rt_multi_create(devices_.data(), (int32_t)devices_.size(), &mg) != RT_OK)
+          return fail(rt_multi_last_error(nullptr));
+        multi_.reset(mg, rt_multi_destroy);
+        multi_devs_ = devices_;
+      }
+      rt_status s = rt_multi_scene_upload(multi_.get(), &desc);
+      if (s == RT_OK) s = rt_multi_render(multi_.get(), &cam, &p, tile_size_, out);
       if (s != RT_OK) {
-        std::string m = rt_multi_last_error(mg);
-        rt_multi_destroy(mg);
+        std::string m = rt_multi_last_error(multi_.get());
+        multi_.reset();
         return fail(m);
       }
-      rt_multi_destroy(mg);
     } else {
-      rt_context* ctx = nullptr;
-      if (rt_context_create(device_, &ctx) != RT_OK) return fail(rt_last_error(nullptr));
+      if (!ctx_ || ctx_dev_ != device_) {  // kept across renders on the same device
+        ctx_.reset();
+        rt_context* c = nullptr;
+        if (rt_context_create(device_, &c) != RT_OK) return fail(rt_last_error(nullptr));
+        ctx_.reset(c, rt_context_destroy);
+        ctx_dev_ = device_;
+      }
       rt_tile tile{0, 0, image_width_, image_height_};
-      rt_status s = rt_scene_upload(ctx, &desc);
-      if (s == RT_OK) s = rt_render_tiles(ctx, &cam, &p, &tile, 1, out, 0, nullptr);
+      rt_status s = rt_scene_upload(ctx_.get(), &desc);
+      if (s == RT_OK) s = rt_render_tiles(ctx_.get(), &cam, &p, &tile, 1, out, 0, nullptr);
       if (s != RT_OK) {
-        std::string m = rt_last_error(ctx);
-        rt_context_destroy(ctx);
+        std::string m = rt_last_error(ctx_.get());
+        ctx_.reset();
         return fail(m);
       }
-      rt_context_destroy(ctx);
     }
     image_.resize(n);
     for (size_t i = 0; i < n; i++)
@@ -228,4 +236,10 @@ class camera {
     last_error_ = m;
     return false;
   }
+  // The device handles of the last render, reused while devices_ / device_ stay the same: a context
+  // per device and, for devices_, one RCCL communicator -- created once, not once per render().
+  std::shared_ptr<rt_multi> multi_;
+  std::vector<int32_t> multi_devs_;
+  std::shared_ptr<rt_context> ctx_;
+  int ctx_dev_ = -1;
 };

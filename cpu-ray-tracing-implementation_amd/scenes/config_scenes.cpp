@@ -3,6 +3,7 @@
 // descriptor camera::render would hand to librt_hip.
 #include "config_scenes.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
@@ -67,8 +68,7 @@ void cornell_box_with_volume(int width, double aspect, config_scene* s) {  // ma
 // center_ = (0,0,0), sphere.h:69); the static variant places each sphere at center1
 // and still draws center2, so the random stream and the sphere list are unchanged.
 void random_motion_ball(int width, double aspect, bool moving, config_scene* s) {
-  std::srand(1);  // the reference never seeds: glibc's default state is srand(1)
-  hittable_list world;
+  hittable_list world;  // rand() from its default state, srand(1) (build_config_scene)
   auto ground = std::make_shared<lambertian>(
       std::make_shared<checker_texture>(color{1.0, 1.0, 1.0}, color{0.6, 0.6, 0.2}, 1.0));
   world.push_back(std::make_shared<sphere>(point3(0, -1000, 0), 1000, ground));
@@ -278,6 +278,11 @@ void glass_fox(int width, double aspect, config_scene* s) {
 }  // namespace
 
 bool build_config_scene(const std::string& name, int width, double aspect, config_scene* out) {
+  // The reference's main() builds one scene per process (main.cc:633-690), so every scene that
+  // draws from rand() -- the perlin / value tables (noise.h:10-136), perlin_texture_ball's box
+  // heights (main.cc:402-437), the RTOW spheres -- starts from glibc's default state, srand(1).
+  // Reseeding here makes a scene independent of the scenes built before it in this process.
+  std::srand(1);
   if (name == "cornell_box")
     cornell_box(width, aspect, out);
   else if (name == "cornell_box_with_volume")
@@ -367,10 +372,12 @@ long long rtsc_gltf_triangles(const char* path, double* xyz, long long cap, char
   }
 }
 
-// The full drop-in path: build the scene, camera::render(of, world, light) to a PPM file; with
-// ndev > 0 the camera renders on `devices` (camera::devices_, the rt_multi_* tiling + RCCL gather).
-int rtsc_render_ppm_on(const char* name, int width, double aspect, int spp, int max_depth, uint64_t seed,
-                       int precision, const int32_t* devices, int ndev, const char* path, char* err, int errlen) {
+// The full drop-in path: build the scene, camera::render(of, world, light) to a PPM file `repeat`
+// times with the same camera (the last render's file is kept); with ndev > 0 the camera renders on
+// `devices` (camera::devices_, the rt_multi_* tiling + RCCL gather).
+int rtsc_render_ppm_repeat(const char* name, int width, double aspect, int spp, int max_depth, uint64_t seed,
+                           int precision, const int32_t* devices, int ndev, int repeat, const char* path, char* err,
+                           int errlen) {
   config_scene s;
   if (devices && ndev > 0) s.cam.devices_.assign(devices, devices + ndev);
   if (!name || !build_config_scene(name, width, aspect, &s)) {
@@ -381,13 +388,21 @@ int rtsc_render_ppm_on(const char* name, int width, double aspect, int spp, int 
   if (max_depth > 0) s.cam.max_recur_depth_ = max_depth;
   s.cam.seed_ = seed;
   s.cam.precision_ = precision == RT_PREC_F64 ? RT_PREC_F64 : RT_PREC_F32;
-  std::ofstream of(path);
-  s.cam.render(of, *s.world, s.light);
-  if (!s.cam.last_error_.empty()) {
-    if (err && errlen > 0) std::snprintf(err, (size_t)errlen, "%s", s.cam.last_error_.c_str());
-    return 2;
+  for (int k = 0; k < std::max(1, repeat); k++) {
+    std::ofstream of(path);
+    s.cam.render(of, *s.world, s.light);
+    if (!s.cam.last_error_.empty()) {
+      if (err && errlen > 0) std::snprintf(err, (size_t)errlen, "%s", s.cam.last_error_.c_str());
+      return 2;
+    }
   }
   return 0;
+}
+
+int rtsc_render_ppm_on(const char* name, int width, double aspect, int spp, int max_depth, uint64_t seed,
+                       int precision, const int32_t* devices, int ndev, const char* path, char* err, int errlen) {
+  return rtsc_render_ppm_repeat(name, width, aspect, spp, max_depth, seed, precision, devices, ndev, 1, path, err,
+                                errlen);
 }
 
 int rtsc_render_ppm(const char* name, int width, double aspect, int spp, int max_depth, uint64_t seed, int precision,

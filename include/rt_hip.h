@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 6
+#define RT_ABI_VERSION 7
 
 typedef enum rt_status {
   RT_OK = 0,
@@ -315,6 +315,9 @@ rt_status rt_multi_stats(rt_multi* m, int32_t rank, rt_counters* out);
  * how many it has, or -1 for invalid arguments. */
 int32_t rt_multi_plan(int32_t width, int32_t height, int32_t ndev, int32_t tile_size, int32_t rank,
                       rt_tile* tiles_out, int32_t cap);
+/* RCCL communicators this process has created (ncclCommInitAll calls by rt_multi_create): a
+ * camera that renders again on the same devices_ keeps its rt_multi, so the count stays put. */
+uint64_t rt_multi_comm_inits(void);
 
 #ifdef __cplusplus
 }

@@ -18,7 +18,7 @@ STRUCTS = ["rt_object", "rt_material", "rt_texture", "rt_scene_desc", "rt_camera
 
 def declared_functions():
     text = open(HDR).read()
-    return sorted(set(re.findall(r"^\s*(?:rt_status|void|const char\*|int32_t|uint32_t)\s+(rt_\w+)\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:rt_status|void|const char\*|int32_t|uint32_t|uint64_t)\s+(rt_\w+)\(", text, re.M)))
 
 
 def test_every_declared_symbol_is_exported():
@@ -28,7 +28,7 @@ def test_every_declared_symbol_is_exported():
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(abi.SIGNATURES), set(names) ^ set(abi.SIGNATURES)
-    assert lib.rt_abi_version() == abi.ABI_VERSION == 6
+    assert lib.rt_abi_version() == abi.ABI_VERSION == 7
 
 
 def test_struct_layout_matches_c(tmp_path):

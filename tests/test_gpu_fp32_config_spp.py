@@ -58,10 +58,9 @@ def test_gloss_fp32_at_config_spp(ctx):
 def test_noise_textures_fp32_at_config_spp(ctx, name):
     # texture.h:80-119 / noise.h: fp32 hit points feed the fp64 noise evaluation
     cs = plugin.ConfigScene(name, 40)
-    # perlin_texture_ball (main.cc:402-437) also has a glass sphere and 400 boxes whose heights come
-    # from the global rand() (so they depend on the scenes built before in the process): a sample
-    # crossing a box edge the other way moves its pixel by ~2/spp (one such pixel of 1,600 at 256 spp
-    # gave RMSE 1.9e-4 in green, the ground's colour), so it runs at 1024 spp
+    # perlin_texture_ball (main.cc:402-437) also has a glass sphere and 400 boxes (heights from rand()
+    # after srand(1), as in the reference's process): a sample crossing a box edge the other way moves
+    # its pixel by ~2/spp, so it runs at 1024 spp
     spp = 1024 if name == "perlin_texture_ball" else 256
     err, div, img, _ = fp32_vs_oracle(ctx, cs.desc, cs.cam, spp, 8, 8)
     check(name, err, div, img.shape[0] * img.shape[1])

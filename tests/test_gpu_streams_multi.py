@@ -160,3 +160,64 @@ def test_camera_render_on_devices_writes_the_same_ppm(tmp_path):
     plugin.render_ppm("cornell_box", c, width=64, spp=8, max_depth=8, seed=6, precision=F32, devices=[0, 0, 0, 0])
     ra, rb, rc = (open(p, "rb").read() for p in (a, b, c))
     assert ra == rb == rc and ra.startswith(b"P3\n64 64\n255\n")
+
+
+def test_camera_keeps_its_communicator_across_renders(tmp_path):
+    # camera::render with devices_ = {0} twice on the same camera: one rt_multi, one ncclCommInitAll
+    lib = abi.load()
+    a, b = str(tmp_path / "once.ppm"), str(tmp_path / "twice.ppm")
+    plugin.render_ppm("cornell_box", a, width=48, spp=8, max_depth=8, seed=2, precision=F32, devices=[0])
+    before = lib.rt_multi_comm_inits()
+    plugin.render_ppm("cornell_box", b, width=48, spp=8, max_depth=8, seed=2, precision=F32, devices=[0], repeat=2)
+    assert lib.rt_multi_comm_inits() - before == 1
+    assert open(a, "rb").read() == open(b, "rb").read()
+    # the single-device camera keeps its context the same way (same image on the second render)
+    c, d = str(tmp_path / "ctx_once.ppm"), str(tmp_path / "ctx_twice.ppm")
+    plugin.render_ppm("cornell_box", c, width=48, spp=8, max_depth=8, seed=2, precision=F32)
+    plugin.render_ppm("cornell_box", d, width=48, spp=8, max_depth=8, seed=2, precision=F32, repeat=3)
+    assert open(c, "rb").read() == open(d, "rb").read() == open(a, "rb").read()
+
+
+def test_scene_copy_of_an_empty_render_is_waited_for(ctx):
+    # the scene copy queued by a render that then exits early (empty tile list) must be
+    # waited for by a device-output render on another stream, which does not copy it again
+    import torch
+    desc, cam, _, _ = scenes.cornell_box(width=64)
+    other, _, _, _ = scenes.cornell_box_with_volume(width=64)
+    ctx.upload(other)
+    ctx.render(cam, 4, 4, seed=1, precision=F32)  # the volume scene resident
+    ctx.upload(desc)
+    want = rt_amd.Context(0)
+    want.upload(desc)
+    ref = want.render(cam, 64, 50, seed=9, precision=F32)
+    want.close()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    p = ctx.params(64, 50, 9, F32)
+    dummy = torch.zeros((1, 3), device="cuda:0")
+    ctx.render_tiles(cam, p, [(0, 0, 0, 0)], dummy.data_ptr(), 1, s1.cuda_stream)  # copies the scene, renders nothing
+    out = torch.full((64 * 64, 3), -1.0, device="cuda:0")
+    ctx.render_tiles(cam, p, [(0, 0, 64, 64)], out.data_ptr(), 1, s2.cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().reshape(ref.shape), ref)
+
+
+def _device_count():
+    import torch
+    return torch.cuda.device_count()
+
+
+@pytest.mark.skipif(_device_count() < 2, reason="needs two GPUs (runs on the first multi-GPU lease)")
+def test_multi_two_devices_rccl_matches_context(ctx):
+    # ncclGather across two distinct devices: rank 1's tiles land in rank 0's buffer in place
+    m = rt_amd.Multi([0, 1])
+    assert m.uses_rccl
+    desc, cam, _, _ = scenes.cornell_box(width=100)
+    m.upload(desc)
+    ctx.upload(desc)
+    for prec in (F32, F64):
+        for ts in (0, 16, 64):
+            got = m.render(cam, 8, 8, seed=5, precision=prec, tile_size=ts)
+            want = ctx.render(cam, 8, 8, seed=5, precision=prec)
+            assert np.array_equal(got, want), (prec, ts)
+    m.close()
