@@ -33,6 +33,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 # 2.4 GHz max clock (MI355X_MICROARCH.md, "Wave scheduling")
 SIMDS, CLOCK_GHZ, VALU_CYCLES = 1024, 2.4, 2
 VALU_PEAK_G = SIMDS * CLOCK_GHZ / VALU_CYCLES  # G wave-instructions/s
+# fp64 issues at half the fp32 vector rate (MI355X spec: 78.6 vs 157.3 TFLOPS vector): a wave64 fp64
+# add / mul / fma / transcendental holds its SIMD 4 cycles, any other VALU instruction 2. The fp64 line's
+# roofline is therefore in SIMD cycles, from the rocprofv3 instruction-mix counters (SQ_INSTS_VALU_*_F64):
+# SQ_ACTIVE_INST_VALU counts one unit per instruction whatever its width (r03a: 59.6 G against 52.9 G
+# instructions on the fp64 kernel, 1.03x on the fp32 one), so it cannot weight fp64 by its issue time.
+F64_CYCLES = 4
+CYCLE_PEAK_G = SIMDS * CLOCK_GHZ  # G SIMD-cycles/s
+F64_MIX = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64")
 # SURVEY.md §8(d) algorithmic bytes: per sample (generate + finalise) and per segment
 B_GEN, B_ACC, B_EXT, B_SHADE = 64, 36, 44, 152
 
@@ -74,7 +82,7 @@ def cpu_threads():
     return n, info
 
 
-def cpu_baseline(scene_name, width, aspect, spp, depth, seed, threads, target_msamples, budget_s=20.0):
+def cpu_baseline(scene_name, width, aspect, spp, depth, seed, threads, target_msamples, budget_s=25.0):
     """The oracle (fp64 restatement of the reference loop, counter RNG) on host cores, over a row sample.
     Returns (the bench line's cpu_baseline object, the rows rendered, their fp64 pixels)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -82,47 +90,63 @@ def cpu_baseline(scene_name, width, aspect, spp, depth, seed, threads, target_ms
     cs = plugin.ConfigScene(scene_name, width, aspect)
     cam = cs.cam
     osc = oracle.from_desc(cs.desc)
+    H, W = cam.image_height, cam.image_width
     # evenly spaced full rows at the full spp and depth: about target_msamples of work, cut to what fits
-    # in budget_s on this host (one row is timed first); progress goes to stderr
-    nrows = max(1, min(cam.image_height, int(target_msamples * 1e6 // (cam.image_width * spp))))
+    # in budget_s on this host (a middle row is timed first: the top rows of a frame can be cheap);
+    # progress goes to stderr
+    nrows = max(1, min(H, int(target_msamples * 1e6 // (W * spp))))
     t0 = time.perf_counter()
-    first, _ = oracle.render(osc, cam, spp, depth, seed=seed, threads=threads, tiles=[(0, 0, cam.image_width, 1)])
+    probe = H // 2
+    first, segs = oracle.render(osc, cam, spp, depth, seed=seed, threads=threads, tiles=[(0, probe, W, 1)])
     t_row = time.perf_counter() - t0
     nrows = max(1, min(nrows, int(budget_s / max(t_row, 1e-6))))
-    step = cam.image_height // nrows
-    rows = list(range(0, cam.image_height, step))[:nrows]
+    rows = sorted(set(int(round(x)) for x in np.linspace(0, H - 1, nrows)))
+    k = min(range(len(rows)), key=lambda i: abs(rows[i] - probe))  # the timed row stands in for its neighbour
+    rows[k] = probe
+    rows = sorted(set(rows))
     print(f"cpu_baseline: one row {t_row:.2f} s, rendering {len(rows)} rows", file=sys.stderr, flush=True)
-    parts = [first.reshape(1, cam.image_width, 3)]
-    for i in range(1, len(rows), 16):
-        batch = rows[i:i + 16]
-        img, _ = oracle.render(osc, cam, spp, depth, seed=seed, threads=threads,
-                               tiles=[(0, y, cam.image_width, 1) for y in batch])
-        parts.append(img.reshape(len(batch), cam.image_width, 3))
-        print(f"cpu_baseline: {i + len(batch)}/{len(rows)} rows, {time.perf_counter() - t0:.1f} s", file=sys.stderr,
+    done = {probe: first.reshape(W, 3)}
+    rest = [y for y in rows if y != probe]
+    for i in range(0, len(rest), 16):
+        batch = rest[i:i + 16]
+        img, sg = oracle.render(osc, cam, spp, depth, seed=seed, threads=threads,
+                                tiles=[(0, y, W, 1) for y in batch])
+        segs += sg
+        for j, y in enumerate(batch):
+            done[y] = img[j * W:(j + 1) * W]
+        print(f"cpu_baseline: {i + len(batch) + 1}/{len(rows)} rows, {time.perf_counter() - t0:.1f} s", file=sys.stderr,
               flush=True)
     dt = time.perf_counter() - t0
-    img = np.concatenate(parts)
-    n = len(rows) * cam.image_width * spp
+    img = np.stack([done[y] for y in rows])
+    n = len(rows) * W * spp
     n_threads, info = threads, buildinfo.host_cpu()
     line = {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": n_threads, "kind": "port",
             "per_core": round(n / dt / 1e6 / n_threads, 4),
+            "segments_per_sample": round(segs / n, 4),
+            "msegments_per_s": round(segs / dt / 1e6, 3),
             "host": info,
             "sample": f"oracle (fp64 C++ restatement of camera.h:135-241, counter RNG, std::thread pool of "
-                      f"{n_threads}) on {len(rows)} rows (every {step}th) x {cam.image_width} px x {spp} spp, "
-                      f"depth {depth}: {n / 1e6:.1f} Msamples in {dt:.1f} s"}
+                      f"{n_threads}) on {len(rows)} evenly spaced rows x {W} px x {spp} spp, "
+                      f"depth {depth}: {n / 1e6:.1f} Msamples ({segs / 1e6:.1f} M segments) in {dt:.1f} s"}
     return line, rows, img
 
 
-def parity_rows(fb, W, rows, ref_rows):
-    """Per-channel RMSE of the GPU framebuffer rows against the oracle's rows (same seed, same sample
-    streams): SURVEY.md §8(c) link 3, at the full bench config."""
+def parity_rows(fb, W, rows, ref_rows, rel_tol=None):
+    """The GPU framebuffer rows against the oracle's rows (same seed, same sample streams): SURVEY.md
+    §8(c) link 3, at the full bench config. fp32: per-channel RMSE < 1e-4 (north_star). fp64 (rel_tol):
+    also the count of pixels differing by more than rel_tol relative (the -m gpu tests hold fp64 to 1e-9)."""
     got = fb.reshape(-1, W, 3)[rows].double().cpu().numpy()
     d = got - ref_rows
     rmse = np.sqrt((d ** 2).reshape(-1, 3).mean(0))
-    return {"rmse": [float(f"{x:.3g}") for x in rmse], "max_abs": float(f"{np.abs(d).max():.3g}"),
-            "rows": len(rows), "pixels": int(d.shape[0] * d.shape[1]), "tolerance": 1e-4,
-            "pass": bool((rmse < 1e-4).all() and np.isfinite(got).all()),
-            "against": "oracle fp64, same seed and counter-RNG streams"}
+    out = {"rmse": [float(f"{x:.3g}") for x in rmse], "max_abs": float(f"{np.abs(d).max():.3g}"),
+           "rows": len(rows), "pixels": int(d.shape[0] * d.shape[1]), "tolerance": 1e-4,
+           "pass": bool((rmse < 1e-4).all() and np.isfinite(got).all()),
+           "against": "oracle fp64, same seed and counter-RNG streams"}
+    if rel_tol is not None:
+        bad = (np.abs(d) > rel_tol * np.maximum(1.0, np.abs(ref_rows))).any(-1)
+        out.update({"rel_tol": rel_tol, "pixels_over_rel_tol": int(bad.sum()),
+                    "max_rel": float(f"{(np.abs(d) / np.maximum(1.0, np.abs(ref_rows))).max():.3g}")})
+    return out
 
 
 def measured_pmc(workload):
@@ -139,9 +163,59 @@ def measured_pmc(workload):
     return found
 
 
-def workload_key(scene_name, W, H, spp, depth, args):
-    return (f"{scene_name} {W}x{H} {spp}spp depth {depth} {args.precision} pool={args.pool} chunk={args.chunk} "
+def workload_key(scene_name, W, H, spp, depth, args, precision=None):
+    return (f"{scene_name} {W}x{H} {spp}spp depth {depth} {precision or args.precision} pool={args.pool} "
+            f"chunk={args.chunk} "
             f"K={args.segments_per_launch} world={args.gpus}" + (" ordered" if args.traversal == "ordered" else ""))
+
+
+def roofline(key, st, segs, my_samples, elapsed, kern, fp64):
+    """The dominant kernel's roofline: VALU issue per launch from the PMC summary of this
+    build and workload (profiles/*_pmc.json) over the launch time measured live with HIP events."""
+    iters, step_ms = st.iterations, st.step_ms
+    if iters <= 0 or step_ms <= 0:
+        return None
+    alg_bytes = (B_GEN + B_ACC) * my_samples + (B_EXT + B_SHADE) * segs
+    avg_s = step_ms / 1e3 / iters
+    mp = measured_pmc(key)
+    roof = {"bound": "valu", "kernel": kern, "unit": "G VALU wave-instr/s", "peak": VALU_PEAK_G,
+            "achieved": None, "frac": None, "traffic": None,
+            "avg_launch_us": round(avg_s * 1e6, 2), "launches": iters,
+            "kernel_share_of_wall": round(step_ms / 1e3 / elapsed, 4),
+            "peak_basis": "1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction",
+            "wavefront_equiv": {"alg_bytes_per_launch": int(alg_bytes / iters),
+                                "GBps": round(alg_bytes / (step_ms / 1e3) / 1e9, 1),
+                                "note": "SURVEY §8(d) bytes a classic SoA wavefront would move for "
+                                        "this work; not HBM traffic"}}
+    if not mp:
+        return roof
+    d = mp[1]
+    c = d.get("counters", {})
+    achieved = d["valu_per_launch"] / avg_s / 1e9
+    roof.update({"achieved": round(achieved, 2), "frac": round(achieved / VALU_PEAK_G, 4),
+                 "valu_per_launch": d["valu_per_launch"], "pmc_source": "profiles/" + mp[0],
+                 "frac_at_measured_clock": d.get("valu_issue_frac_measured_clock"),
+                 "lane_valu_per_segment": round(d["valu_per_launch"] * 64 / (segs / iters), 1),
+                 "valu_lane_util": d.get("valu_lane_util"), "wait_frac": d.get("wait_frac")})
+    if fp64 and all(k in c for k in F64_MIX):
+        # issue time weighted by width: fp64 instructions hold the SIMD twice as long
+        n64 = sum(c[k] for k in F64_MIX)
+        cycles = VALU_CYCLES * (d["valu_per_launch"] - n64) + F64_CYCLES * n64
+        ach = cycles / avg_s / 1e9
+        roof.update({"unit": "G SIMD-cycles/s", "peak": CYCLE_PEAK_G, "achieved": round(ach, 2),
+                     "frac": round(ach / CYCLE_PEAK_G, 4), "frac_unweighted": round(achieved / VALU_PEAK_G, 4),
+                     "fp64_instr_per_launch": n64, "valu_cycles_per_launch": cycles,
+                     "peak_basis": "1024 SIMDs x 2.4 GHz; VALU cycles = 2 per wave64 instruction, 4 per fp64 "
+                                   "add/mul/fma/transcendental (SQ_INSTS_VALU_*_F64; fp64 vector rate = 1/2 fp32)"})
+    if roof["valu_lane_util"] is not None:  # issued lanes that do work: idle lanes of a divergent wave do not
+        roof["useful_frac"] = round(roof["frac"] * roof["valu_lane_util"], 4)
+    if d.get("hbm_bytes_per_launch") is not None:
+        tb = d["hbm_bytes_per_launch"]
+        roof["traffic"] = int(tb)
+        roof["hbm"] = {"achieved_GBps": round(tb / avg_s / 1e9, 2), "peak_GBps": HBM_PEAK_GBS,
+                       "frac": round(tb / avg_s / 1e9 / HBM_PEAK_GBS, 5)}
+    assert roof["frac"] <= 1.0, roof
+    return roof
 
 
 def main():
@@ -164,7 +238,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: the CPUs this process may use, capped by the "
                                                                    "box's share (cgroup quota / OMP_NUM_THREADS)")
-    ap.add_argument("--cpu-msamples", type=float, default=240.0,
+    ap.add_argument("--cpu-msamples", type=float, default=600.0,
                     help="size of the CPU-baseline row sample (Msamples of oracle work)")
     ap.add_argument("--f64-steps", type=int, default=3,
                     help="after the headline run, time this many frames of the fp64 path (the reference's "
@@ -254,13 +328,10 @@ def main():
         segs_total = float(s.item())
     total_samples = W * H * spp * args.steps
     value = total_samples / elapsed / 1e6
-    f64_line = None
+    kern = "k_step" if args.segments_per_launch > 0 else "k_persist"
+    f64_run = None
     if args.f64_steps > 0 and prec == abi.RT_PREC_F32:
-        e64, st64, _ = run(abi.RT_PREC_F64, args.f64_steps, 1, False)
-        f64_line = {"value": round(W * H * spp * args.f64_steps / e64 / 1e6, 2), "unit": "Msamples/s",
-                    "steps": args.f64_steps, "ms_per_step": round(e64 / args.f64_steps * 1e3, 3),
-                    "dtype": "fp64", "note": "the same frames on the fp64 path (the reference's precision, "
-                                             "vec3.h:7), timed the same way after the headline run"}
+        f64_run = run(abi.RT_PREC_F64, args.f64_steps, 1, args.kernel_timing == "on")
 
     if rank == 0:
         my_samples = counts[0] * spp * args.steps
@@ -269,42 +340,34 @@ def main():
         # dominant kernel of rank 0 (k_persist: the persistent extend+shade loop, one launch per frame;
         # k_step with --segments-per-launch K: the fused wavefront step), average launch duration from HIP
         # events on the render stream. It is VALU-issue bound: path state stays in registers, so HBM
-        # moves ~0.1 % of the classic wavefront's bytes. achieved = VALU wave-instructions per launch
-        # (rocprofv3 SQ_INSTS_VALU of this build and workload, profiles/*_pmc.json) / live launch time.
+        # moves ~0.1 % of the classic wavefront's bytes. achieved = VALU work per launch (rocprofv3
+        # counters of this build and workload, profiles/*_pmc.json) / live launch time.
         roof = None
-        if args.kernel_timing == "on" and iters > 0:
-            alg_bytes = (B_GEN + B_ACC) * my_samples + (B_EXT + B_SHADE) * segs
-            avg_s = step_ms / 1e3 / iters
-            kern = "k_step" if args.segments_per_launch > 0 else "k_persist"
-            mp = measured_pmc(key)
-            roof = {"bound": "valu", "kernel": kern, "unit": "G VALU wave-instr/s", "peak": VALU_PEAK_G,
-                    "achieved": None, "frac": None, "traffic": None,
-                    "avg_launch_us": round(avg_s * 1e6, 2), "launches": iters,
-                    "kernel_share_of_wall": round(step_ms / 1e3 / elapsed, 4),
-                    "peak_basis": "1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction",
-                    "wavefront_equiv": {"alg_bytes_per_launch": int(alg_bytes / iters),
-                                        "GBps": round(alg_bytes / (step_ms / 1e3) / 1e9, 1),
-                                        "note": "SURVEY §8(d) bytes a classic SoA wavefront would move for "
-                                                "this work; not HBM traffic"}}
-            if mp:
-                d = mp[1]
-                achieved = d["valu_per_launch"] / avg_s / 1e9
-                roof.update({"achieved": round(achieved, 2), "frac": round(achieved / VALU_PEAK_G, 4),
-                             "valu_per_launch": d["valu_per_launch"], "pmc_source": "profiles/" + mp[0],
-                             "frac_at_measured_clock": d.get("valu_issue_frac_measured_clock"),
-                             "lane_valu_per_segment": round(d["valu_per_launch"] * 64 / (segs / iters), 1)})
-                if d.get("hbm_bytes_per_launch") is not None:
-                    tb = d["hbm_bytes_per_launch"]
-                    roof["traffic"] = int(tb)
-                    roof["hbm"] = {"achieved_GBps": round(tb / avg_s / 1e9, 2), "peak_GBps": HBM_PEAK_GBS,
-                                   "frac": round(tb / avg_s / 1e9 / HBM_PEAK_GBS, 5)}
-                assert roof["frac"] <= 1.0, roof
+        if args.kernel_timing == "on":
+            roof = roofline(key, st, segs, my_samples, elapsed, kern, prec == abi.RT_PREC_F64)
         cpu = parity = None
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or cpu_threads()[0]
             cpu, rows, ref_rows = cpu_baseline(scene_name, width, aspect, spp, depth, args.seed, threads,
                                                args.cpu_msamples)
             parity = parity_rows(fb, W, rows, ref_rows)
+        f64_line = None
+        if f64_run is not None:
+            e64, st64, fb64 = f64_run
+            v64 = W * H * spp * args.f64_steps / e64 / 1e6
+            s64 = st64.segments / max(1, counts[0] * spp * args.f64_steps)
+            f64_line = {"value": round(v64, 2), "unit": "Msamples/s", "steps": args.f64_steps,
+                        "ms_per_step": round(e64 / args.f64_steps * 1e3, 3), "dtype": "fp64",
+                        "segments_per_sample": round(s64, 4),
+                        "note": "the same frames on the fp64 path (the reference's precision, vec3.h:7), timed the "
+                                "same way after the headline run"}
+            if args.kernel_timing == "on":
+                f64_line["roofline"] = roofline(workload_key(scene_name, W, H, spp, depth, args, "f64"), st64,
+                                                st64.segments, counts[0] * spp * args.f64_steps, e64, kern, True)
+            if cpu:
+                f64_line["parity"] = parity_rows(fb64, W, rows, ref_rows, rel_tol=1e-9)
+                f64_line["speedup_vs_cpu_baseline"] = round(v64 / cpu["value"], 1)
+                f64_line["speedup_per_segment"] = round(v64 * s64 / (cpu["value"] * cpu["segments_per_sample"]), 1)
         line = {
             "metric": "Msamples/sec (pixels*spp) Cornell Box 800x800@1024spp; 1/2/4/8-GPU scaling"
             if args.config == "c2" else f"Msamples/sec (pixels*spp) {scene_name} {W}x{H}@{spp}spp",
@@ -325,6 +388,10 @@ def main():
         }
         if cpu:
             line["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
+            # per unit of work: the GPU stops zero-throughput paths, the oracle does not, so
+            # it traces more segments per sample
+            line["speedup_per_segment"] = round(value * seg_per_sample / (cpu["value"] * cpu["segments_per_sample"]),
+                                                1)
         print(json.dumps(line), flush=True)
     ctx.close()
     if world > 1:

@@ -61,14 +61,15 @@ __device__ __forceinline__ float fdiv_inv(float a, float b, float inv_b) {
 __device__ __forceinline__ double fdiv_inv(double a, double b, double) { return a / b; }
 __device__ __forceinline__ double fsqrt(double x) { return sqrt(x); }
 __device__ __forceinline__ double flog(double x) { return log(x); }
-// sin(2*pi*u), cos(2*pi*u); the fp64 form evaluates phi = 2*pi*u first like utility.h:36,64
-__device__ __forceinline__ void sincos2pi(double u, double& s, double& c) {
-  double phi = 2 * 3.1415926535897932385 * u;
-  s = sin(phi);
-  c = cos(phi);
-}
+// sin(2*pi*u), cos(2*pi*u) for u in [0, 1) (utility.h:36,64 evaluate sin(phi) of phi = 2*pi*u).
+// fp64: sincospi(2u) -- 2u is exact, and the reduction is an exact subtraction, so there is no
+// Payne-Hanek path: OCML's general sin/cos carry one, whose registers (the kernel's budget is its
+// heaviest path) held the fp64 kernels at 2-3 waves per SIMD. Within an ulp or two of
+// sin(fl(2 pi u)): far inside the fp64 parity tolerance (1e-9 relative against the oracle).
+__device__ __forceinline__ void sincos2pi(double u, double& s, double& c) { sincospi(2.0 * u, &s, &c); }
 __device__ __forceinline__ float pow5(float x) { return (x * x) * (x * x) * x; }
-__device__ __forceinline__ double pow5(double x) { return pow(x, 5.0); }
+// material.h:131 std::pow(1 - cosine, 5), as products (a few ulp; OCML's pow is a log/exp pair)
+__device__ __forceinline__ double pow5(double x) { return (x * x) * (x * x) * x; }
 
 // ------------------------------------------------------------------ vectors
 template <class R>
@@ -223,8 +224,8 @@ struct DevScene {
   const Light<R>* light;
   const LinRec<R>* lin;  // linear program (n_linear > 0)
   uint32_t n_linear;
-  const FlatQuad* flatq;  // flat program (fp32, has_flat): quads grouped by plane axis, then boxes
-  const FlatBox* flatb;
+  const FlatQuadT<R>* flatq;  // flat program (has_flat): quads grouped by plane axis, then boxes
+  const FlatBoxT<R>* flatb;
   uint32_t n_flatq[3], n_flatb;
   int32_t has_flat;
   uint32_t root;
@@ -1089,37 +1090,55 @@ __device__ __forceinline__ void trace_linear(const DevScene<R>& sc, V<R> wo, V<R
   t_best = tmax;
 }
 
-// ------------------------------------------------------------------ flat program (fp32)
-// rt_scene.h FlatQuad / FlatBox: world-space axis-aligned quads in three branch-free loops
+// ------------------------------------------------------------------ flat program
+// rt_scene.h FlatQuadT / FlatBoxT: world-space axis-aligned quads in three branch-free loops
 // (one per plane axis, records scalar-loaded in pairs), then the slab tests of the boxes.
 // A quad is the aquad_t test (quad.h:30-64 for n = +-e_A); the record index of the closest
-// hit is kept and turned into (entry, instance) once at the end.
+// hit is kept and turned into (entry, instance) once at the end. fp64 (round 3): the same
+// program with the per-ray reciprocal 1/d in IEEE double, so a quad costs multiplies instead
+// of the three fp64 divisions of the ordered linear program.
+template <class R>
 struct FlatQuad2 {
-  FlatQuad a, b;
+  FlatQuadT<R> a, b;
 };
-template <int A>
-__device__ __forceinline__ void flat_quad_test(const FlatQuad& r, int32_t idx, V<float> o, V<float> d,
-                                               V<float> inv, float tmin, float& tmax, int32_t& best,
-                                               uint64_t xkey) {
+// 1/d for the flat program: v_rcp_f32 in fp32 (as rcp3), IEEE division in fp64
+template <class R>
+__device__ __forceinline__ V<R> flat_inv(V<R> d) {
+  if constexpr (sizeof(R) == 4)
+    return rcp3(d);
+  else
+    return mkv(R(1) / d.x, R(1) / d.y, R(1) / d.z);
+}
+template <int A, class R>
+__device__ __forceinline__ void flat_quad_test(const FlatQuadT<R>& r, int32_t idx, V<R> o, V<R> d, V<R> inv,
+                                               R tmin, R& tmax, int32_t& best, uint64_t xkey) {
   constexpr int U = A == 0 ? 1 : 0, W = A == 2 ? 1 : 2;
-  const float th = (r.plane - comp<A>(o)) * comp<A>(inv);
-  const float a = ((comp<U>(o) + th * comp<U>(d)) - r.lo_u) * r.inv_u;
-  const float b = ((comp<W>(o) + th * comp<W>(d)) - r.lo_w) * r.inv_w;
-  const uint32_t lo = __float_as_uint(tmin);
-  const bool in_t = __float_as_uint(th) - lo <= __float_as_uint(tmax) - lo;
-  const bool in_ab = max(__float_as_uint(a), __float_as_uint(b)) <= 0x3f800000u;
+  const R th = (r.plane - comp<A>(o)) * comp<A>(inv);
+  const R a = ((comp<U>(o) + th * comp<U>(d)) - r.lo_u) * r.inv_u;
+  const R b = ((comp<W>(o) + th * comp<W>(d)) - r.lo_w) * r.inv_w;
+  bool in_t, in_ab;
+  if constexpr (sizeof(R) == 4) {
+    const uint32_t lo = __float_as_uint(tmin);
+    in_t = __float_as_uint(th) - lo <= __float_as_uint(tmax) - lo;
+    in_ab = max(__float_as_uint(a), __float_as_uint(b)) <= 0x3f800000u;
+  } else {  // the same order tricks on the 64-bit patterns (non-negative doubles order like their bits)
+    const uint64_t lo = (uint64_t)__double_as_longlong(tmin);
+    in_t = (uint64_t)__double_as_longlong(th) - lo <= (uint64_t)__double_as_longlong(tmax) - lo;
+    const uint64_t ua = (uint64_t)__double_as_longlong(a), ub = (uint64_t)__double_as_longlong(b);
+    in_ab = (ua > ub ? ua : ub) <= 0x3FF0000000000000ull;
+  }
   const uint64_t key = ((uint64_t)(uint32_t)r.inst << 32) | r.e;
   const bool h = in_t & in_ab & (key != xkey);
   tmax = h ? th : tmax;
   best = h ? idx : best;
 }
-template <int A>
-__device__ __forceinline__ void flat_quads(const FlatQuad* q, uint32_t n, int32_t base, V<float> o, V<float> d,
-                                           V<float> inv, float tmin, float& tmax, int32_t& best, uint64_t xkey) {
-  const FlatQuad2* q2 = reinterpret_cast<const FlatQuad2*>(q);
+template <int A, class R>
+__device__ __forceinline__ void flat_quads(const FlatQuadT<R>* q, uint32_t n, int32_t base, V<R> o, V<R> d,
+                                           V<R> inv, R tmin, R& tmax, int32_t& best, uint64_t xkey) {
+  const FlatQuad2<R>* q2 = reinterpret_cast<const FlatQuad2<R>*>(q);
 #pragma unroll 1
   for (uint32_t k = 0; k < n; k += 2) {
-    const FlatQuad2 r = ld_uniform(q2, k >> 1);
+    const FlatQuad2<R> r = ld_uniform(q2, k >> 1);
     flat_quad_test<A>(r.a, base + (int32_t)k, o, d, inv, tmin, tmax, best, xkey);
     flat_quad_test<A>(r.b, base + (int32_t)k + 1, o, d, inv, tmin, tmax, best, xkey);
   }
@@ -1129,31 +1148,33 @@ __device__ __forceinline__ void flat_quads(const FlatQuad* q, uint32_t n, int32_
 // (excl_i == inst; the face is excl_e & 7, rt_scene.h) starts on that face's plane: its
 // distance to it becomes -inf, i.e. the plane is behind the ray whichever way it goes --
 // a ray going out then has tf < 0 (no hit), one going in exits through another face.
+template <class R>
 struct Slab {
-  float t0[3], t1[3], tn, tf, th;
+  R t0[3], t1[3], tn, tf, th;
 };
-__device__ __forceinline__ Slab flat_slab(const FlatBox& b, V<float> o, V<float> inv, float tmin, int32_t excl_i,
-                                          uint32_t xf) {
-  Slab s;
+template <class R>
+__device__ __forceinline__ Slab<R> flat_slab(const FlatBoxT<R>& b, V<R> o, V<R> inv, R tmin, int32_t excl_i,
+                                             uint32_t xf) {
+  Slab<R> s;
   const bool left = excl_i == b.inst;
-  const float ninf = -Num<float>::inf();
+  const R ninf = -Num<R>::inf();
   s.t0[0] = (left & (xf == 0)) ? ninf : (b.lo[0] - o.x) * inv.x;
   s.t1[0] = (left & (xf == 1)) ? ninf : (b.hi[0] - o.x) * inv.x;
   s.t0[1] = (left & (xf == 2)) ? ninf : (b.lo[1] - o.y) * inv.y;
   s.t1[1] = (left & (xf == 3)) ? ninf : (b.hi[1] - o.y) * inv.y;
   s.t0[2] = (left & (xf == 4)) ? ninf : (b.lo[2] - o.z) * inv.z;
   s.t1[2] = (left & (xf == 5)) ? ninf : (b.hi[2] - o.z) * inv.z;
-  s.tn = fmaxf(fmaxf(fminf(s.t0[0], s.t1[0]), fminf(s.t0[1], s.t1[1])), fminf(s.t0[2], s.t1[2]));
-  s.tf = fminf(fminf(fmaxf(s.t0[0], s.t1[0]), fmaxf(s.t0[1], s.t1[1])), fmaxf(s.t0[2], s.t1[2]));
+  s.tn = fmax(fmax(fmin(s.t0[0], s.t1[0]), fmin(s.t0[1], s.t1[1])), fmin(s.t0[2], s.t1[2]));
+  s.tf = fmin(fmin(fmax(s.t0[0], s.t1[0]), fmax(s.t0[1], s.t1[1])), fmax(s.t0[2], s.t1[2]));
   s.th = s.tn >= tmin ? s.tn : s.tf;
   return s;
 }
-__device__ __forceinline__ void trace_flat(const DevScene<float>& sc, V<float> o, V<float> d, uint32_t excl_e,
-                                           int32_t excl_i, float& t_best, uint32_t& e_best, int32_t& i_best,
-                                           uint32_t& nm) {
-  const float tmin = 0.001f;
-  float tmax = Num<float>::inf();
-  const V<float> inv = rcp3(d);
+template <class R>
+__device__ __forceinline__ void trace_flat(const DevScene<R>& sc, V<R> o, V<R> d, uint32_t excl_e, int32_t excl_i,
+                                           R& t_best, uint32_t& e_best, int32_t& i_best, uint32_t& nm) {
+  const R tmin = R(0.001);
+  R tmax = Num<R>::inf();
+  const V<R> inv = flat_inv(d);
   const uint64_t xkey = ((uint64_t)(uint32_t)excl_i << 32) | excl_e;
   const uint32_t xf = excl_e & 7u;
   int32_t best = -1;
@@ -1163,8 +1184,8 @@ __device__ __forceinline__ void trace_flat(const DevScene<float>& sc, V<float> o
   flat_quads<2>(sc.flatq + n0 + n1, n2, (int32_t)(n0 + n1), o, d, inv, tmin, tmax, best, xkey);
 #pragma unroll 1
   for (uint32_t k = 0; k < sc.n_flatb; k++) {
-    const FlatBox b = ld_uniform(sc.flatb, k);
-    const Slab s = flat_slab(b, o, inv, tmin, excl_i, xf);
+    const FlatBoxT<R> b = ld_uniform(sc.flatb, k);
+    const Slab<R> s = flat_slab(b, o, inv, tmin, excl_i, xf);
     const bool h = (s.tn <= s.tf) & (s.th >= tmin) & (s.th <= tmax);
     tmax = h ? s.th : tmax;
     best = h ? (int32_t)(nq + k) : best;
@@ -1175,7 +1196,7 @@ __device__ __forceinline__ void trace_flat(const DevScene<float>& sc, V<float> o
   nm = 0;
   if (best < 0) return;
   if ((uint32_t)best < nq) {
-    const FlatQuad& r = sc.flatq[best];
+    const FlatQuadT<R>& r = sc.flatq[best];
     e_best = r.e;
     i_best = r.inst;
     nm = r.nm;
@@ -1183,19 +1204,19 @@ __device__ __forceinline__ void trace_flat(const DevScene<float>& sc, V<float> o
   }
   // the face of the box: the axis whose slab bound is the hit distance (recomputed exactly
   // as in the loop), on the side the ray enters (or leaves, from inside)
-  const FlatBox& b = sc.flatb[(uint32_t)best - nq];
-  const Slab s = flat_slab(b, o, inv, tmin, excl_i, xf);
+  const FlatBoxT<R>& b = sc.flatb[(uint32_t)best - nq];
+  const Slab<R> s = flat_slab(b, o, inv, tmin, excl_i, xf);
   const bool enter = s.tn >= tmin;
   int k = 2;
   if (enter) {
-    if (s.tn == fminf(s.t0[0], s.t1[0])) k = 0;
-    else if (s.tn == fminf(s.t0[1], s.t1[1])) k = 1;
+    if (s.tn == fmin(s.t0[0], s.t1[0])) k = 0;
+    else if (s.tn == fmin(s.t0[1], s.t1[1])) k = 1;
   } else {
-    if (s.tf == fmaxf(s.t0[0], s.t1[0])) k = 0;
-    else if (s.tf == fmaxf(s.t0[1], s.t1[1])) k = 1;
+    if (s.tf == fmax(s.t0[0], s.t1[0])) k = 0;
+    else if (s.tf == fmax(s.t0[1], s.t1[1])) k = 1;
   }
-  const float dk = k == 0 ? d.x : (k == 1 ? d.y : d.z);
-  const int side = enter ? (dk < 0.f ? 1 : 0) : (dk < 0.f ? 0 : 1);
+  const R dk = k == 0 ? d.x : (k == 1 ? d.y : d.z);
+  const int side = enter ? (dk < R(0) ? 1 : 0) : (dk < R(0) ? 0 : 1);
   e_best = b.face[2 * k + side];
   i_best = b.inst;
   nm = b.mat | (uint32_t)k << 28 | ((b.neg >> (2 * k + side)) & 1u) << 31;

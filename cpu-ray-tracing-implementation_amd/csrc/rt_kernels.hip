@@ -748,21 +748,25 @@ struct LinearTrav {
     trace_linear<R, SPH, TRI, VOL>(sc, s.o, s.d, s.tm, s.xe, s.xi, k, (uint32_t)s.bounce, t, e, i);
   }
 };
-// The flat program (fp32, quad/box scenes such as every Cornell config): rt_device.h trace_flat.
+// The flat program (quad/box scenes such as every Cornell config): rt_device.h trace_flat.
 #ifndef RT_FLAT_WAVES
 #define RT_FLAT_WAVES 7
 #endif
+#ifndef RT_FLAT_WAVES_F64  // fp64 flat program: waves per SIMD the register budget is cut for (1: none)
+#define RT_FLAT_WAVES_F64 4
+#endif
+template <class R>
 struct FlatTrav {
   static constexpr int kStack = 0;
-  static constexpr int kWaves = RT_FLAT_WAVES;
+  static constexpr int kWaves = sizeof(R) == 4 ? RT_FLAT_WAVES : RT_FLAT_WAVES_F64;
   static constexpr int kLdsNodes = 0;
   static constexpr bool kFlat = true;
   static constexpr bool kWide = false;
-  static constexpr bool kColdLds = false;  // 72 -> 64 VGPRs, but C2 23.5 -> 24.1 ms/frame
+  static constexpr bool kColdLds = false;  // fp32: 72 -> 64 VGPRs, but C2 23.5 -> 24.1 ms/frame
   template <class PS>
-  __device__ __forceinline__ static void run(const DevScene<float>& sc, const Node<float>*, const PS& s,
-                                             Keys, uint32_t*, float& t, uint32_t& e, int32_t& i, uint32_t& nm) {
-    trace_flat(sc, s.o, s.d, s.xe, s.xi, t, e, i, nm);
+  __device__ __forceinline__ static void run(const DevScene<R>& sc, const Node<R>*, const PS& s, Keys, uint32_t*,
+                                             R& t, uint32_t& e, int32_t& i, uint32_t& nm) {
+    trace_flat<R>(sc, s.o, s.d, s.xe, s.xi, t, e, i, nm);
   }
 };
 // LDSN: the scene's BVH nodes (at most kLdsNodeMax) are copied into LDS at kernel start, so
@@ -1344,8 +1348,8 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
   s.lin = (const LinRec<R>*)at(h.off_linear);
   s.n_linear = h.n_linear;
   s.has_flat = (int32_t)h.has_flat;
-  s.flatq = (const FlatQuad*)at(h.off_flat_quad);
-  s.flatb = (const FlatBox*)at(h.off_flat_box);
+  s.flatq = (const FlatQuadT<R>*)at(h.off_flat_quad);
+  s.flatb = (const FlatBoxT<R>*)at(h.off_flat_box);
   for (int a = 0; a < 3; a++) s.n_flatq[a] = h.n_flat_quad[a];
   s.n_flatb = h.n_flat_box;
   s.root = h.root;
@@ -1458,12 +1462,10 @@ void launch_k(const Params<R>& p, uint32_t grid, hipStream_t st) {
 template <class R>
 void launch_step(const Params<R>& p, int stack, bool sph, bool tri, uint32_t grid, hipStream_t st) {
   const bool vol = p.sc.has_volumes != 0;
-  if constexpr (sizeof(R) == 4) {
-    // the flat program (world-space quads and boxes); the extended kernels keep the linear one
-    if (p.sc.has_flat && p.cam_mode == RT_CAM_PERSPECTIVE && !p.sc.has_procedural) {
-      launch_k<float, FlatTrav>(p, grid, st);
-      return;
-    }
+  // the flat program (world-space quads and boxes, fp32 and fp64); the extended kernels keep the linear one
+  if (p.sc.has_flat && p.cam_mode == RT_CAM_PERSPECTIVE && !p.sc.has_procedural) {
+    launch_k<R, FlatTrav<R>>(p, grid, st);
+    return;
   }
   if (p.sc.n_linear > 0) {
     if (!sph && !tri && !vol)

@@ -68,38 +68,46 @@ struct alignas(16) LinRec {
 };
 static_assert(3 * kMaxChain <= 14, "an instance chain must fit one LinRec");
 
-// The *flat program* (fp32 kernels only): a linear program whose ops are all axis-aligned
-// quads, at world level or under translate-only instances, is rewritten in world space
-// (translations folded into the records) and regrouped by plane axis, so a wave runs three
-// branch-free loops with no per-op dispatch. An instance holding exactly the six quads of
-// `box()` (quad.h:91-112) with one lambertian material becomes one slab-test record. Order
-// inside the scene only decides exact-t ties, which fp32 does not reproduce anyway; the fp64
-// path keeps the reference-ordered linear program.
-//   FlatQuad, group A (plane axis): U < W are the two other axes,
+// The *flat program*: a linear program whose ops are all axis-aligned quads, at world level or
+// under translate-only instances, is rewritten in world space (translations folded into the
+// records) and regrouped by plane axis, so a wave runs three branch-free loops with no per-op
+// dispatch. An instance holding exactly the six quads of `box()` (quad.h:91-112) with one
+// lambertian material becomes one slab-test record. Both blobs carry it (FlatQuadT<float> /
+// <double>): the fp32 kernels use it by default; the fp64 kernels too (round 3), where it agrees
+// with the reference-ordered linear program up to rounding (t as (plane - o_A) * (1/d_A) instead
+// of a division per quad); RT_TRAV_ORDERED keeps the linear program. Order inside the scene only
+// decides exact-t ties.
+//   FlatQuadT, group A (plane axis): U < W are the two other axes,
 //     alpha = (o_U + t d_U - lo_u) * inv_u, beta = (o_W + t d_W - lo_w) * inv_w (signed inv);
 //   groups are padded to an even count with records whose plane is NaN (never hit).
 //   nm (both records) = what shade needs of the hit: material | A << 28 | (n_A < 0) << 31, the
 //   quad's outward normal being +-e_A exactly (translations leave normals alone).
-struct alignas(16) FlatQuad {
-  float plane, lo_u, lo_w, inv_u;
-  float inv_w;
+template <class R>
+struct alignas(16) FlatQuadT {
+  R plane, lo_u, lo_w, inv_u;
+  R inv_w;
   uint32_t e;    // the quad's entry (exclusion state; its record is not read again)
   int32_t inst;  // its instance (translate-only), -1 at world level
   uint32_t nm;
 };
+using FlatQuad = FlatQuadT<float>;
 constexpr uint32_t kNmMat = (1u << 28) - 1u;
-//   FlatBox: the slab [lo, hi]; face[2k + s] is the entry of the face on plane lo_k (s = 0)
+//   FlatBoxT: the slab [lo, hi]; face[2k + s] is the entry of the face on plane lo_k (s = 0)
 //   or hi_k (s = 1); the compiler gives the faces quad records at an 8-aligned index, face f
 //   at base + f, so a ray leaving the box knows the plane it starts on (trace_flat).
-struct alignas(16) FlatBox {
-  float lo[3];
+template <class R>
+struct alignas(16) FlatBoxT {
+  R lo[3];
+  R hi[3];
   int32_t inst;
-  float hi[3];
   uint32_t mat;
   uint32_t face[6];
   uint32_t neg;  // bit f: face f's outward normal points to -e_k
   uint32_t pad;
 };
+using FlatBox = FlatBoxT<float>;
+static_assert(sizeof(FlatQuadT<float>) == 32 && sizeof(FlatQuadT<double>) == 64, "flat quad records");
+static_assert(sizeof(FlatBoxT<float>) == 64 && sizeof(FlatBoxT<double>) == 96, "flat box records");
 
 // quad.h:9-23 precomputed: n = unit(cross(u,v)), D = dot(n, corner),
 // a = cross(v, w), b = cross(w, u) with w = cross(u,v)/dot(cross(u,v),cross(u,v)),
@@ -268,9 +276,9 @@ struct SceneHeader {
   uint64_t n_images;
   uint64_t bytes;
   uint32_t n_linear;  // 0: no linear program (use the BVH traversal)
-  uint32_t n_flat_box;          // flat program (fp32 blob only): boxes
+  uint32_t n_flat_box;          // flat program: boxes
   uint32_t n_flat_quad[3];      // flat program: quads per plane axis (even counts)
-  uint32_t has_flat;            // 1: the flat program replaces the linear program in fp32
+  uint32_t has_flat;            // 1: the flat program replaces the linear program (RT_TRAV_AUTO)
   uint64_t off_flat_quad, off_flat_box;
   uint32_t n_quads, n_spheres, n_tris, n_volumes, n_nodes, n_refs, n_mats, n_texs;
   // wide BVH (fp32 blob only; has_wide = 0: none)

@@ -194,8 +194,8 @@ class Compiler {
   Item bvh(std::vector<Item>& items, size_t b, size_t e, int depth);
   int make_instance(const std::vector<Op>& chain, uint32_t blas);
   LinRec<double> lin_record(uint32_t op) const;
-  bool flat_program(const std::vector<uint32_t>& lin, std::vector<FlatQuad>& quads, uint32_t nq[3],
-                    std::vector<FlatBox>& boxes);
+  bool flat_program(const std::vector<uint32_t>& lin, std::vector<FlatQuadT<double>>& quads, uint32_t nq[3],
+                    std::vector<FlatBoxT<double>>& boxes);
   bool wide_bvh(const std::vector<Item>& prims, CompiledScene* out);
   bool box_of_quads(const std::vector<Item>& prims, double lo[3], double hi[3]) const;
   std::vector<int> aligned_;  // per quad: 1 + perm for axis-aligned quads, 0 otherwise
@@ -825,11 +825,11 @@ LinRec<double> Compiler::lin_record(uint32_t op) const {
   return r;
 }
 
-// The flat program of rt_scene.h (fp32 kernels): the linear program's ops are all
-// axis-aligned quads, at world level or in translate-only instances. Returns false (no flat
-// program) for anything else.
-bool Compiler::flat_program(const std::vector<uint32_t>& lin, std::vector<FlatQuad>& quads, uint32_t nq[3],
-                            std::vector<FlatBox>& boxes) {
+// The flat program of rt_scene.h: the linear program's ops are all axis-aligned quads, at world
+// level or in translate-only instances. Returns false (no flat program) for anything else. The
+// records come out in double (the fp64 blob) and are rounded once for the fp32 blob (flat32).
+bool Compiler::flat_program(const std::vector<uint32_t>& lin, std::vector<FlatQuadT<double>>& quads, uint32_t nq[3],
+                            std::vector<FlatBoxT<double>>& boxes) {
   struct Q {
     uint32_t e;
     int32_t inst;
@@ -852,14 +852,14 @@ bool Compiler::flat_program(const std::vector<uint32_t>& lin, std::vector<FlatQu
     }
     return true;
   };
-  std::vector<FlatQuad> grp[3];
+  std::vector<FlatQuadT<double>> grp[3];
   auto add_quad = [&](const Q& q, const double* off) {
-    FlatQuad r{};
-    r.plane = (float)(q.plane + off[q.A]);
-    r.lo_u = (float)(q.lo_u + off[q.U]);
-    r.lo_w = (float)(q.lo_w + off[q.W]);
-    r.inv_u = (float)(1.0 / q.len_u);
-    r.inv_w = (float)(1.0 / q.len_w);
+    FlatQuadT<double> r{};
+    r.plane = q.plane + off[q.A];
+    r.lo_u = q.lo_u + off[q.U];
+    r.lo_w = q.lo_w + off[q.W];
+    r.inv_u = 1.0 / q.len_u;
+    r.inv_w = 1.0 / q.len_w;
     r.e = q.e;
     r.inst = q.inst;
     const Quad<double>& qq = quads_[epay(q.e)];
@@ -867,7 +867,7 @@ bool Compiler::flat_program(const std::vector<uint32_t>& lin, std::vector<FlatQu
     grp[q.A].push_back(r);
   };
   // six quads of box() (quad.h:91-112) with one lambertian material -> one slab record
-  auto as_box = [&](const std::vector<Q>& qs, const double* off, FlatBox& b) {  // b.face: original entries
+  auto as_box = [&](const std::vector<Q>& qs, const double* off, FlatBoxT<double>& b) {  // b.face: original entries
     if (qs.size() != 6) return false;
     const int32_t mat = quads_[epay(qs[0].e)].mat;
     if (mats_[(size_t)mat].kind != M_LAMBERTIAN) return false;
@@ -893,8 +893,8 @@ bool Compiler::flat_program(const std::vector<uint32_t>& lin, std::vector<FlatQu
       if (quads_[epay(q.e)].n[q.A] < 0) b.neg |= 1u << f;
     }
     for (int k = 0; k < 3; k++) {
-      b.lo[k] = (float)(lo[k] + off[k]);
-      b.hi[k] = (float)(hi[k] + off[k]);
+      b.lo[k] = lo[k] + off[k];
+      b.hi[k] = hi[k] + off[k];
     }
     b.inst = qs[0].inst;
     b.mat = (uint32_t)mat;
@@ -934,7 +934,7 @@ bool Compiler::flat_program(const std::vector<uint32_t>& lin, std::vector<FlatQu
       qs.push_back(q);
     }
     if (k == lin.size()) return undo();
-    FlatBox b{};
+    FlatBoxT<double> b{};
     if (as_box(qs, off, b)) {
       // the faces get copies of their quad records at an 8-aligned index, face j at base + j:
       // a ray leaving the box knows from its entry which slab plane it starts on (trace_flat)
@@ -959,9 +959,9 @@ bool Compiler::flat_program(const std::vector<uint32_t>& lin, std::vector<FlatQu
   quads.clear();
   for (int a = 0; a < 3; a++) {
     if (grp[a].size() % 2) {  // pad to pairs: a NaN plane never hits
-      FlatQuad pad{};
+      FlatQuadT<double> pad{};
       pad.nm = (uint32_t)a << 28;
-      pad.plane = std::numeric_limits<float>::quiet_NaN();
+      pad.plane = std::numeric_limits<double>::quiet_NaN();
       pad.e = kNoHit;
       pad.inst = -2;
       grp[a].push_back(pad);
@@ -1394,14 +1394,14 @@ bool Compiler::run(CompiledScene* out, std::string* err) {
   std::vector<LinRec<double>> linear;
   if (lin_top.lin_ok)
     for (uint32_t op : lin_top.lin) linear.push_back(lin_record(op));
-  // the flat program of the fp32 blob, when the linear program has that form (may add quad records)
-  std::vector<FlatQuad> fq;
-  std::vector<FlatBox> fb;
+  // the flat program of both blobs, when the linear program has that form (may add quad records)
+  std::vector<FlatQuadT<double>> fq;
+  std::vector<FlatBoxT<double>> fb;
   uint32_t nq[3] = {0, 0, 0};
   out->desc_quads = (int)quads_.size();
   const bool has_flat = lin_top.lin_ok && !lin_top.lin.empty() && flat_program(lin_top.lin, fq, nq, fb);
   if (has_flat) {
-    for (const FlatQuad& q : fq) out->flat_quads += q.inst != -2;
+    for (const FlatQuadT<double>& q : fq) out->flat_quads += q.inst != -2;
     out->flat_boxes = (int)fb.size();
   }
   out->stack_need = std::max(1, root.need);
@@ -1412,13 +1412,33 @@ bool Compiler::run(CompiledScene* out, std::string* err) {
   out->hdr = pack(out->blob32, map32(quads_), map32(spheres_), map32(tris_), map32(insts_), map32(vols_),
                   map32(nodes_), refs_, map32(mats_), map32(texs_), to32(light_), map32(linear), texdata_, images_);
   if (has_flat) {
-    out->hdr.off_flat_quad = append(out->blob32, fq);
-    out->hdr.off_flat_box = append(out->blob32, fb);
-    out->blob32.resize((out->blob32.size() + 255) & ~size_t(255));
-    out->hdr.bytes = out->blob32.size();
-    for (int a = 0; a < 3; a++) out->hdr.n_flat_quad[a] = nq[a];
-    out->hdr.n_flat_box = (uint32_t)fb.size();
-    out->hdr.has_flat = 1;
+    std::vector<FlatQuadT<float>> fq32;
+    std::vector<FlatBoxT<float>> fb32;
+    for (const FlatQuadT<double>& q : fq)
+      fq32.push_back({(float)q.plane, (float)q.lo_u, (float)q.lo_w, (float)q.inv_u, (float)q.inv_w, q.e, q.inst, q.nm});
+    for (const FlatBoxT<double>& b : fb) {
+      FlatBoxT<float> r{};
+      for (int k = 0; k < 3; k++) {
+        r.lo[k] = (float)b.lo[k];
+        r.hi[k] = (float)b.hi[k];
+      }
+      r.inst = b.inst;
+      r.mat = b.mat;
+      for (int f = 0; f < 6; f++) r.face[f] = b.face[f];
+      r.neg = b.neg;
+      fb32.push_back(r);
+    }
+    auto put = [&](std::vector<unsigned char>& blob, SceneHeader& h, const auto& q, const auto& b) {
+      h.off_flat_quad = append(blob, q);
+      h.off_flat_box = append(blob, b);
+      blob.resize((blob.size() + 255) & ~size_t(255));
+      h.bytes = blob.size();
+      for (int a = 0; a < 3; a++) h.n_flat_quad[a] = nq[a];
+      h.n_flat_box = (uint32_t)b.size();
+      h.has_flat = 1;
+    };
+    put(out->blob32, out->hdr, fq32, fb32);
+    put(out->blob64, out->hdr64, fq, fb);
   }
   // the wide BVH (fp32) when the world is a BVH over world-level primitives only
   bool prims_only = etype(root.entry) == E_NODE;
