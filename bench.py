@@ -224,7 +224,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)  # 10 frames: 0.25 s on one GPU, 36 ms over 8
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
+    # the headline computes in fp64, the reference's precision (vec3.h:7); the fp32 production path, which
+    # meets north_star's per-channel RMSE < 1e-4, is timed after it as the "alt" line
+    ap.add_argument("--precision", default="f64", choices=["f32", "f64"])
     ap.add_argument("--pool", type=int, default=0, help="path slots / persistent lanes (0 = library default)")
     ap.add_argument("--chunk", type=int, default=0, help="samples per work item (0 = library default)")
     ap.add_argument("--segments-per-launch", type=int, default=0,
@@ -240,9 +242,9 @@ def main():
                                                                    "box's share (cgroup quota / OMP_NUM_THREADS)")
     ap.add_argument("--cpu-msamples", type=float, default=600.0,
                     help="size of the CPU-baseline row sample (Msamples of oracle work)")
-    ap.add_argument("--f64-steps", type=int, default=3,
-                    help="after the headline run, time this many frames of the fp64 path (the reference's "
-                         "precision, vec3.h:7) on the same config; 0 = skip")
+    ap.add_argument("--alt-steps", "--f64-steps", type=int, default=10, dest="alt_steps",
+                    help="after the headline run, time this many frames of the other precision on the same "
+                         "config (f32 after an f64 headline and vice versa); 0 = skip")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -329,9 +331,11 @@ def main():
     total_samples = W * H * spp * args.steps
     value = total_samples / elapsed / 1e6
     kern = "k_step" if args.segments_per_launch > 0 else "k_persist"
-    f64_run = None
-    if args.f64_steps > 0 and prec == abi.RT_PREC_F32:
-        f64_run = run(abi.RT_PREC_F64, args.f64_steps, 1, args.kernel_timing == "on")
+    alt_name = "f32" if args.precision == "f64" else "f64"
+    alt_prec = abi.RT_PREC_F32 if alt_name == "f32" else abi.RT_PREC_F64
+    alt_run = None
+    if args.alt_steps > 0:
+        alt_run = run(alt_prec, args.alt_steps, 1, args.kernel_timing == "on")
 
     if rank == 0:
         my_samples = counts[0] * spp * args.steps
@@ -350,24 +354,28 @@ def main():
             threads = args.cpu_threads or cpu_threads()[0]
             cpu, rows, ref_rows = cpu_baseline(scene_name, width, aspect, spp, depth, args.seed, threads,
                                                args.cpu_msamples)
-            parity = parity_rows(fb, W, rows, ref_rows)
-        f64_line = None
-        if f64_run is not None:
-            e64, st64, fb64 = f64_run
-            v64 = W * H * spp * args.f64_steps / e64 / 1e6
-            s64 = st64.segments / max(1, counts[0] * spp * args.f64_steps)
-            f64_line = {"value": round(v64, 2), "unit": "Msamples/s", "steps": args.f64_steps,
-                        "ms_per_step": round(e64 / args.f64_steps * 1e3, 3), "dtype": "fp64",
-                        "segments_per_sample": round(s64, 4),
-                        "note": "the same frames on the fp64 path (the reference's precision, vec3.h:7), timed the "
-                                "same way after the headline run"}
+            parity = parity_rows(fb, W, rows, ref_rows, rel_tol=1e-9 if prec == abi.RT_PREC_F64 else None)
+        alt_line = None
+        if alt_run is not None:
+            ea, sta, fba = alt_run
+            va = W * H * spp * args.alt_steps / ea / 1e6
+            sa = sta.segments / max(1, counts[0] * spp * args.alt_steps)
+            alt_line = {"value": round(va, 2), "unit": "Msamples/s", "steps": args.alt_steps,
+                        "ms_per_step": round(ea / args.alt_steps * 1e3, 3),
+                        "dtype": "fp64" if alt_name == "f64" else "fp32", "segments_per_sample": round(sa, 4),
+                        "note": ("the same frames on the fp32 production path (north_star: per-channel RMSE < 1e-4 "
+                                 "against the fp64 reference), timed the same way after the headline run"
+                                 if alt_name == "f32" else
+                                 "the same frames on the fp64 path (the reference's precision, vec3.h:7), timed "
+                                 "the same way after the headline run")}
             if args.kernel_timing == "on":
-                f64_line["roofline"] = roofline(workload_key(scene_name, W, H, spp, depth, args, "f64"), st64,
-                                                st64.segments, counts[0] * spp * args.f64_steps, e64, kern, True)
+                alt_line["roofline"] = roofline(workload_key(scene_name, W, H, spp, depth, args, alt_name), sta,
+                                                sta.segments, counts[0] * spp * args.alt_steps, ea, kern,
+                                                alt_name == "f64")
             if cpu:
-                f64_line["parity"] = parity_rows(fb64, W, rows, ref_rows, rel_tol=1e-9)
-                f64_line["speedup_vs_cpu_baseline"] = round(v64 / cpu["value"], 1)
-                f64_line["speedup_per_segment"] = round(v64 * s64 / (cpu["value"] * cpu["segments_per_sample"]), 1)
+                alt_line["parity"] = parity_rows(fba, W, rows, ref_rows, rel_tol=1e-9 if alt_name == "f64" else None)
+                alt_line["speedup_vs_cpu_baseline"] = round(va / cpu["value"], 1)
+                alt_line["speedup_per_segment"] = round(va * sa / (cpu["value"] * cpu["segments_per_sample"]), 1)
         line = {
             "metric": "Msamples/sec (pixels*spp) Cornell Box 800x800@1024spp; 1/2/4/8-GPU scaling"
             if args.config == "c2" else f"Msamples/sec (pixels*spp) {scene_name} {W}x{H}@{spp}spp",
@@ -384,7 +392,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "parity": parity,
-            "f64": f64_line,
+            alt_name: alt_line,
         }
         if cpu:
             line["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)

@@ -22,7 +22,8 @@ namespace rtd {
 #define RT_WIDE_SPEC 1
 #endif
 
-// Math policy. fp64 (the parity path): IEEE division/sqrt and libm, as the reference.
+// Math policy. fp64 (the parity path): libm where the reference calls it (log), and division,
+// reciprocal and square root refined from the hardware estimates to about an ulp (below).
 // fp32 (the production path): the hardware ops -- v_rcp_f32, v_sqrt_f32, v_rsq_f32,
 // v_log_f32, and v_sin_f32 / v_cos_f32, which take their argument in revolutions, so
 // sin(2*pi*u) for u in [0,1) needs no range reduction.
@@ -48,9 +49,48 @@ __device__ __forceinline__ void sincos2pi(float u, float& s, float& c) {
   c = cosf(phi);
 }
 #endif
-__device__ __forceinline__ double fdiv(double a, double b) { return a / b; }
-// a / b given inv_b = rcp3(..) of b computed once per ray: bit-identical to fdiv(a, b)
-// (fp64 and the precise build divide; rcp3 then returns nothing the compiler keeps)
+// fp64 division, reciprocal and square root (round 3). IEEE fp64 division on gfx950 is a
+// v_div_scale / v_rcp / 5 x v_fma / v_div_fmas / v_div_fixup sequence, and sqrt a similar one: the
+// fp64 Cornell kernel spent ~60 % of its fp64 instructions in ~32 of them per segment (r03c counters:
+// 35 v_rcp/v_rsq per lane-segment). Here: the hardware estimate (v_rcp_f64 / v_rsq_f64, ~2^-23
+// relative) refined by Newton-Raphson to within an ulp or two of the IEEE result -- far inside the
+// fp64 parity tolerance against the oracle (1e-9 relative; measured ~1e-15). Zero, infinite and NaN
+// operands, where the refinement would turn an exact infinity into NaN, fall back to the raw
+// estimate, which v_rcp / v_rsq compute exactly for them (1/0 = inf, 1/inf = 0, rsq(0) = inf).
+__device__ __forceinline__ double frcp(double b) {
+  const double r0 = __builtin_amdgcn_rcp(b);
+  double r = r0;
+  double e = fma(-b, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-b, r, 1.0);
+  r = fma(r, e, r);
+  return __builtin_isfinite(r) ? r : r0;
+}
+__device__ __forceinline__ double fdiv(double a, double b) {
+  const double r = frcp(b);
+  const double q = a * r;
+  const double res = fma(fma(-b, q, a), r, q);  // one residual step: ~correctly rounded
+  return __builtin_isfinite(res) ? res : q;     // a/0, inf/b, 0/0 as IEEE
+}
+__device__ __forceinline__ double frsq(double x) {  // 1/sqrt(x)
+  const double r0 = __builtin_amdgcn_rsq(x);
+  const double h = 0.5 * x;
+  double r = r0;
+  r = r * fma(-h * r, r, 1.5);
+  r = r * fma(-h * r, r, 1.5);
+  return __builtin_isfinite(r) ? r : r0;
+}
+__device__ __forceinline__ double fsqrt(double x) {
+  const double r = __builtin_amdgcn_rsq(x);
+  double g = x * r, h = 0.5 * r;
+  const double e = fma(-g, h, 0.5);  // Goldschmidt step
+  g = fma(g, e, g);
+  h = fma(h, e, h);
+  g = fma(fma(-g, g, x), h, g);  // residual correction
+  return (x > 0.0 && x < __builtin_huge_val()) ? g : (x >= 0.0 ? x : __builtin_nan(""));
+}
+// a / b given inv_b = rcp3(..) of b computed once per ray: bit-identical to fdiv(a, b) in fp32
+// (the precise build divides; rcp3 then returns nothing the compiler keeps)
 __device__ __forceinline__ float fdiv_inv(float a, float b, float inv_b) {
 #ifndef RT_PRECISE_F32
   return a * inv_b;
@@ -58,8 +98,7 @@ __device__ __forceinline__ float fdiv_inv(float a, float b, float inv_b) {
   return a / b;
 #endif
 }
-__device__ __forceinline__ double fdiv_inv(double a, double b, double) { return a / b; }
-__device__ __forceinline__ double fsqrt(double x) { return sqrt(x); }
+__device__ __forceinline__ double fdiv_inv(double a, double b, double) { return fdiv(a, b); }
 __device__ __forceinline__ double flog(double x) { return log(x); }
 // sin(2*pi*u), cos(2*pi*u) for u in [0, 1) (utility.h:36,64 evaluate sin(phi) of phi = 2*pi*u).
 // fp64: sincospi(2u) -- 2u is exact, and the reduction is an exact subtraction, so there is no
@@ -67,6 +106,9 @@ __device__ __forceinline__ double flog(double x) { return log(x); }
 // heaviest path) held the fp64 kernels at 2-3 waves per SIMD. Within an ulp or two of
 // sin(fl(2 pi u)): far inside the fp64 parity tolerance (1e-9 relative against the oracle).
 __device__ __forceinline__ void sincos2pi(double u, double& s, double& c) { sincospi(2.0 * u, &s, &c); }
+// x / pi (pdf.h:27-29 cosine_pdf::value): fp32 as before, fp64 as a product with 1/pi
+__device__ __forceinline__ float div_pi(float x) { return fdiv(x, 3.14159265358979323846f); }
+__device__ __forceinline__ double div_pi(double x) { return x * 0.318309886183790671537767526745; }
 __device__ __forceinline__ float pow5(float x) { return (x * x) * (x * x) * x; }
 // material.h:131 std::pow(1 - cosine, 5), as products (a few ulp; OCML's pow is a log/exp pair)
 __device__ __forceinline__ double pow5(double x) { return (x * x) * (x * x) * x; }
@@ -108,9 +150,15 @@ template <class R>
 __device__ __forceinline__ V<R> operator*(V<R> a, R c) {
   return {a.x * c, a.y * c, a.z * c};
 }
+__device__ __forceinline__ double frcp(double b);
 template <class R>
 __device__ __forceinline__ V<R> operator/(V<R> a, R c) {
-  return {a.x / c, a.y / c, a.z / c};
+  if constexpr (sizeof(R) == 8) {  // one reciprocal for the three (within ~1.5 ulp of each quotient)
+    const R r = frcp(c);
+    return {a.x * r, a.y * r, a.z * r};
+  } else {
+    return {a.x / c, a.y / c, a.z / c};
+  }
 }
 template <class R>
 __device__ __forceinline__ R dot(V<R> a, V<R> b) {  // vec3.h:61
@@ -146,8 +194,8 @@ __device__ __forceinline__ V<float> unit(V<float> a) {  // vec3.h:77 (v / |v|), 
   return a * frsq(a.x * a.x + a.y * a.y + a.z * a.z);
 }
 template <>
-__device__ __forceinline__ V<double> unit(V<double> a) {  // vec3.h:77
-  return a / len(a);
+__device__ __forceinline__ V<double> unit(V<double> a) {  // vec3.h:77 (v / |v|), as v * rsqrt(v.v) refined
+  return a * frsq(a.x * a.x + a.y * a.y + a.z * a.z);
 }
 
 template <class R>
@@ -298,7 +346,7 @@ __device__ __forceinline__ V<R> box_inv(V<R> d) {
   if constexpr (sizeof(R) == 4)
     return mkv(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
   else
-    return mkv(R(1) / d.x, R(1) / d.y, R(1) / d.z);
+    return mkv(frcp(d.x), frcp(d.y), frcp(d.z));
 }
 
 // Ray/box slab test with IEEE min/max (a NaN slab is ignored: conservative) and
@@ -338,11 +386,11 @@ __device__ __forceinline__ bool tri_test(V<R> p0, V<R> e1, V<R> e2, V<R> o, V<R>
   V<R> s1 = cross(d, e2), s2 = cross(s, e1);
   R inv = fdiv(R(1), dot(s1, e1));
   R th = dot(s2, e2) * inv, b0 = dot(s1, s) * inv, b1 = dot(s2, d) * inv;
-  if (sizeof(R) == 8) {  // the parity path divides like triangle.h:14
+  if constexpr (sizeof(R) == 8) {  // the parity path divides like triangle.h:14
     R den = dot(s1, e1);
-    th = dot(s2, e2) / den;
-    b0 = dot(s1, s) / den;
-    b1 = dot(s2, d) / den;
+    th = fdiv(dot(s2, e2), den);
+    b0 = fdiv(dot(s1, s), den);
+    b1 = fdiv(dot(s2, d), den);
   }
   if (th < tmin || th > tmax) return false;
   if (b0 < R(0) || b1 < R(0) || b0 + b1 > R(1)) return false;
@@ -378,8 +426,8 @@ __device__ __forceinline__ bool sphere_roots(T ox, T oy, T oz, T dx, T dy, T dz,
     T disc = b * b - T(4) * a * c;
     if (disc < T(0)) return false;
     T sq = fsqrt(disc);
-    lo = (-b - sq) / (T(2) * a);
-    hi = (-b + sq) / (T(2) * a);
+    lo = fdiv(-b - sq, T(2) * a);
+    hi = fdiv(-b + sq, T(2) * a);
   } else {
     T ia = fdiv(T(1), a);
     T bh = -(dx * fx + dy * fy + dz * fz);  // -b/2
@@ -513,8 +561,8 @@ __device__ __forceinline__ bool aquad_t(const R* f, V<R> o, V<R> d, V<R> inv, R 
   R pv = (comp<W>(o) + th * comp<W>(d)) - f[2];
   R a, b;
   if constexpr (sizeof(R) == 8) {
-    a = pu / f[5];
-    b = pv / f[6];
+    a = fdiv(pu, f[5]);
+    b = fdiv(pv, f[6]);
   } else {
     a = pu * f[3];
     b = pv * f[4];
@@ -882,7 +930,6 @@ __device__ __forceinline__ bool trace_wide(const DevScene<float>& sc, const unsi
   // ms/frame; the LDS-resident C3 tree, whose node visits are cheap and whose leaves hold up to 6
   // spheres, lost (62.2 -> 63.6: nodes visited past a postponed leaf are not culled by its hits).
   if constexpr (!LDSN && RT_WIDE_SPEC) {
-  (void)keep_going;
   bool have = true;  // cur holds a node or a leaf still to visit
   for (;;) {
     uint32_t leaf = 0u;  // the postponed leaf (a leaf code is never 0)
@@ -946,6 +993,12 @@ __device__ __forceinline__ bool trace_wide(const DevScene<float>& sc, const unsi
     if (!have) {
       done = true;
       break;
+    }
+    if constexpr (PAUSE < 64) {
+      // active-ray control: once PAUSE of the lanes that entered have finished (__ballot count), the
+      // others pause with their state in (cur, sp, tmax, e_best) and the LDS stack, the finished ones
+      // are shaded and start their next rays, and the wave traverses again at full width
+      if ((uint32_t)__popcll(__ballot(1)) <= keep_going) break;
     }
   }
   } else {
@@ -1107,7 +1160,7 @@ __device__ __forceinline__ V<R> flat_inv(V<R> d) {
   if constexpr (sizeof(R) == 4)
     return rcp3(d);
   else
-    return mkv(R(1) / d.x, R(1) / d.y, R(1) / d.z);
+    return mkv(frcp(d.x), frcp(d.y), frcp(d.z));
 }
 template <int A, class R>
 __device__ __forceinline__ void flat_quad_test(const FlatQuadT<R>& r, int32_t idx, V<R> o, V<R> d, V<R> inv,

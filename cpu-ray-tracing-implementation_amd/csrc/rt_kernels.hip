@@ -660,7 +660,7 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
           R u1 = U();
           R u2 = U();
           dir = iso ? unit(on_sphere(u1, u2)) : onb_transform(b, cosine_dir(u1, u2));
-          pv = iso ? iso_pdf : fmax(R(0), fdiv(dot(unit(dir), b.y), Num<R>::pi()));
+          pv = iso ? iso_pdf : fmax(R(0), div_pi(dot(unit(dir), b.y)));
         } else {  // dual_pdf(hittable_pdf(light), material pdf) (camera.h:227-239, pdf.h:48-61)
           R c = U();
           R u1 = U();
@@ -670,7 +670,7 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
             dir = light_random(Lt, pw, u1, u2);
           else
             dir = iso ? unit(on_sphere(u1, u2)) : onb_transform(b, cosine_dir(u1, u2));
-          R mp = iso ? iso_pdf : fmax(R(0), fdiv(dot(unit(dir), b.y), Num<R>::pi()));
+          R mp = iso ? iso_pdf : fmax(R(0), div_pi(dot(unit(dir), b.y)));
           pv = R(0.5) * light_pdf(Lt, pw, dir, from_light) + R(0.5) * mp;
         }
         R ps;
@@ -678,7 +678,7 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
           ps = iso_pdf;
         } else {
           R c = dot(n, unit(dir));
-          ps = c < R(0) ? R(0) : fdiv(c, Num<R>::pi());
+          ps = c < R(0) ? R(0) : div_pi(c);
         }
         if constexpr (sizeof(R) == 8)
           s.thr = s.thr * ((att * ps) / pv);  // camera.h:238 grouping on the parity path
@@ -806,7 +806,10 @@ struct StackTrav {
 #define RT_WIDE_RELOAD 0
 #endif
 #ifndef RT_SHADE_BATCH  // < 64: a wave stops traversing to shade once this many of its lanes have finished
-#define RT_SHADE_BATCH 64  // (measured on C3: 16 / 32 / 48 are 1-2 % slower than never pausing)
+#define RT_SHADE_BATCH 64  // (LDS-resident tree; measured on C3: 16 / 32 / 48 are 1-2 % slower than never pausing)
+#endif
+#ifndef RT_SHADE_BATCH_GLOBAL  // the same for trees in HBM (speculative traversal)
+#define RT_SHADE_BATCH_GLOBAL 64
 #endif
 template <bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN>
 struct WideTrav {
@@ -845,7 +848,7 @@ struct WideTrav {
   __device__ __forceinline__ static bool steps(const DevScene<float>& sc, const Node<float>* lds, const PS& s,
                                                StackT* stk, WideRay& ry) {
     const unsigned char* base = (const unsigned char*)lds;
-    return trace_wide<SPH, TRI, QUAD, MOV, LDSN, kBlock, RT_SHADE_BATCH>(
+    return trace_wide<SPH, TRI, QUAD, MOV, LDSN, kBlock, LDSN ? RT_SHADE_BATCH : RT_SHADE_BATCH_GLOBAL>(
         sc, base, (const float4*)(base + sc.n_wnodes * kWNodeLdsStride), s.o, s.d, s.tm, s.xe, stk, ry);
   }
 };

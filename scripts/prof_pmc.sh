@@ -13,5 +13,7 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAIT_A
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE -d $out/pmc2 -o run --output-format csv -- python3 $B > $out/pmc2.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS -d $out/pmc3 -o run --output-format csv -- python3 $B > $out/pmc3.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH -d $out/pmc4 -o run --output-format csv -- python3 $B > $out/pmc4.log 2>&1
+# the VALU instruction mix: fp64 instructions issue at half the fp32 rate (bench.py's fp64 roofline)
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 -d $out/pmc5 -o run --output-format csv -- python3 $B > $out/pmc5.log 2>&1
 key=$(python3 -c "import json; print([json.loads(l) for l in open('$out/trace.log') if l.startswith('{\"metric')][-1]['config']['key'])")
 python3 scripts/pmc_summary.py $out $tag "$key" $out/summary

@@ -73,6 +73,18 @@ def test_defocus_blur_fp32_at_config_spp(ctx):
     check("defocus", err, div, img.shape[0] * img.shape[1])
 
 
+def test_skybox_fisheye_fp32_at_config_spp(ctx, tmp_path, monkeypatch):
+    # main.cc:173-183: the fisheye camera (camera.h:259-275) looking at a glass sphere (refraction index 1)
+    # under a picture-texture skybox (camera.h:180-190) at 256 spp; the skybox is written as a PFM here
+    # (the reference's bathroom.exr is not in its checkout)
+    from test_plugin import _write_assets
+    _write_assets(tmp_path)
+    monkeypatch.setenv("RT_ASSETS", str(tmp_path))
+    cs = plugin.ConfigScene("skybox_and_fisheye", 40)
+    err, div, img, _ = fp32_vs_oracle(ctx, cs.desc, cs.cam, 256, 5, 3)
+    check("skybox_fisheye", err, div, img.shape[0] * img.shape[1])
+
+
 def test_earthmap_fp32_at_config_spp(ctx, monkeypatch):
     # main.cc:185-196: the reference's earthmap.jpg on the moving sphere, magenta skybox
     monkeypatch.setenv("RT_ASSETS", GOLDEN_ASSETS)

@@ -340,18 +340,30 @@ def test_picture_texture_on_quads_matches_oracle(ctx):
 
 
 def test_full_c2_fp32_matches_fp64(ctx):
-    # BASELINE config 2 at full size: the fp32 production path against the fp64 device path
+    # BASELINE config 2 at full size (800x800, 1024 spp, depth 50) against the oracle: 8 evenly spaced
+    # full rows (6.6 M samples) rendered by the fp64 restatement of the reference loop with the same
+    # seed and sample streams; fp32 to north_star's per-channel RMSE < 1e-4, fp64 to 1e-9 relative
     cs = plugin.ConfigScene("cornell_box", 800)
     ctx.upload(cs.desc)
     a = ctx.render(cs.cam, 1024, 50, seed=1, precision=F32).astype(np.float64)
     b = ctx.render(cs.cam, 1024, 50, seed=1, precision=F64)
     # 2e9 segments: rare rounding events (a light sample on the light's edge) must not become NaN
     assert np.isfinite(a).all(), np.argwhere(~np.isfinite(a).all(-1))[:5]
+    assert np.isfinite(b).all(), np.argwhere(~np.isfinite(b).all(-1))[:5]
+    rows = [int(round(y)) for y in np.linspace(0, 799, 8)]
+    ref, _ = oracle.render(oracle.from_desc(cs.desc), cs.cam, 1024, 50, seed=1, threads=16,
+                           tiles=[(0, y, 800, 1) for y in rows])
+    ref = ref.reshape(len(rows), 800, 3)
+    err32 = rmse(a[rows], ref)
+    assert (err32 < 1e-4).all(), err32
+    rel = np.abs(b[rows] - ref) / np.maximum(1.0, np.abs(ref))
+    # fp64 follows the oracle's paths; a path may leave it only where an ulp decides an edge (not seen
+    # at this size), and then it moves one pixel by ~value/spp
+    assert (rel > 1e-9).any(-1).sum() <= 2, (float(rel.max()), int((rel > 1e-9).any(-1).sum()))
+    assert (rmse(b[rows], ref) < 1e-6).all(), rmse(b[rows], ref)
+    # the whole frame: fp32 against fp64
     assert (rmse(a, b) < 1e-4).all(), rmse(a, b)
-    # resolution-independent property: the image mean matches a small oracle render's
-    sc, cam, _, _ = oracle.builtin("cornell_box", 100)
-    ref, _ = oracle.render(sc, cam, 256, 50, seed=9)
-    np.testing.assert_allclose(b.reshape(-1, 3).mean(0), ref.reshape(-1, 3).mean(0), rtol=0.02)
+    print(f"full C2 rows vs oracle: fp32 rmse {err32}, fp64 max rel {rel.max():.3g}")
 
 
 def test_edge_cases(ctx):
