@@ -289,12 +289,18 @@ struct DevScene {
   uint32_t n_wnodes, n_wprim_words, wroot, wide_stack, wide_kinds;
   int32_t has_wide;
   uint32_t wide_big;  // primitives at the head of the word stream, tested before the tree
+  const WNode8* wnodes8;  // the compressed 8-wide tree over the same leaves (has_wide8)
+  uint32_t wroot8, wide8_stack;
+  int32_t has_wide8;
   // a tree in HBM keeps at most kWideLdsStack stack entries per lane in LDS; deeper entries (rare:
   // every child of every node on a path hit) go to wide_spill[(depth - kWideLdsStack) * spill_lanes + lane]
   uint32_t* wide_spill;
   uint32_t spill_lanes;
 };
-constexpr uint32_t kWideLdsStack = 24;
+#ifndef RT_WIDE_LDS_STACK
+#define RT_WIDE_LDS_STACK 24
+#endif
+constexpr uint32_t kWideLdsStack = RT_WIDE_LDS_STACK;
 
 // World -> object through an instance chain (hittable.h:75-82, 125-135, 192-202, 259-270).
 template <class R>
@@ -849,10 +855,60 @@ __host__ __device__ __forceinline__ uint32_t wide_code16(uint32_t c) {
 }
 template <bool LDSN>
 using WStackT = typename std::conditional<LDSN, uint16_t, uint32_t>::type;
-template <bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN, int BLOCK, int PAUSE>
+// slab distances of the 8 children of a compressed node (rt_scene.h WNode8) as sort keys
+// (bits(t_near) with the slot in the low 3 bits; 0xFFFFFFFF: missed or unused). A plane's distance
+// is fma(q, s * inv, (o_node - o) * inv): the quantum and origin are folded into the ray once per
+// node, so a child plane costs one byte conversion (v_cvt_f32_ubyte) and one fma.
+__device__ __forceinline__ void wide8_keys(const WNode8* node, V<float> o, V<float> inv, float tmin, float tmax,
+                                           uint32_t k[8], uint4& c0, uint4& c1) {
+  const uint4* nd = (const uint4*)node;
+  const uint4 h = nd[0], qa = nd[1], qb = nd[2], qc = nd[3];
+  c0 = nd[4];
+  c1 = nd[5];
+  const float ax = __uint_as_float((h.w & 0xFFu) << 23) * inv.x, bx = (__uint_as_float(h.x) - o.x) * inv.x;
+  const float ay = __uint_as_float(((h.w >> 8) & 0xFFu) << 23) * inv.y, by = (__uint_as_float(h.y) - o.y) * inv.y;
+  const float az = __uint_as_float(((h.w >> 16) & 0xFFu) << 23) * inv.z, bz = (__uint_as_float(h.z) - o.z) * inv.z;
+  const uint32_t n = h.w >> 24;
+  // qlo x: qa.x (slots 0-3), qa.y (4-7); y: qa.z, qa.w; z: qb.x, qb.y. qhi x: qb.z, qb.w; y: qc.x, qc.y; z: qc.z, qc.w
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    const int sh = 8 * (c & 3);
+    const bool hi4 = c >= 4;
+    auto q = [&](uint32_t w) { return (float)((w >> sh) & 0xFFu); };
+    const float tx0 = fmaf(q(hi4 ? qa.y : qa.x), ax, bx), tx1 = fmaf(q(hi4 ? qb.w : qb.z), ax, bx);
+    const float ty0 = fmaf(q(hi4 ? qa.w : qa.z), ay, by), ty1 = fmaf(q(hi4 ? qc.y : qc.x), ay, by);
+    const float tz0 = fmaf(q(hi4 ? qb.y : qb.x), az, bz), tz1 = fmaf(q(hi4 ? qc.w : qc.z), az, bz);
+    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
+    const float tf =
+        fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax)) * Num<float>::box_slack();
+    k[c] = ((uint32_t)c < n && tn <= tf) ? ((__float_as_uint(tn) & ~7u) | (uint32_t)c) : 0xFFFFFFFFu;
+  }
+  // sort near to far: the 19-comparator network for 8 inputs
+#define RT_CS8(a, b)                          \
+  {                                           \
+    const uint32_t lo_ = min(k[a], k[b]);     \
+    k[b] = max(k[a], k[b]);                   \
+    k[a] = lo_;                               \
+  }
+  RT_CS8(0, 2) RT_CS8(1, 3) RT_CS8(4, 6) RT_CS8(5, 7)
+  RT_CS8(0, 4) RT_CS8(1, 5) RT_CS8(2, 6) RT_CS8(3, 7)
+  RT_CS8(0, 1) RT_CS8(2, 3) RT_CS8(4, 5) RT_CS8(6, 7)
+  RT_CS8(2, 4) RT_CS8(3, 5)
+  RT_CS8(1, 4) RT_CS8(3, 6)
+  RT_CS8(1, 2) RT_CS8(3, 4) RT_CS8(5, 6)
+#undef RT_CS8
+}
+// the child code in slot (key & 7) of the node whose codes are c0 (slots 0-3) and c1 (4-7)
+__device__ __forceinline__ uint32_t wide8_child(uint32_t key, const uint4& c0, const uint4& c1) {
+  const uint4 c = (key & 4u) ? c1 : c0;
+  const uint32_t lo = (key & 1u) ? c.y : c.x, hi = (key & 1u) ? c.w : c.z;
+  return (key & 2u) ? hi : lo;
+}
+template <bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN, int BLOCK, int PAUSE, bool W8 = false>
 __device__ __forceinline__ bool trace_wide(const DevScene<float>& sc, const unsigned char* lds_nodes,
                                            const float4* lds_prims, V<float> o, V<float> d, float time,
                                            uint32_t excl_e, WStackT<LDSN>* stk, WideRay& ry) {
+  static_assert(!W8 || (!LDSN && RT_WIDE_SPEC), "the 8-wide nodes are traversed speculatively, from HBM");
   constexpr uint32_t kLeafBit = LDSN ? kWLeaf16 : kWLeaf;
   const float tmin = 0.001f;
   const V<float> inv = box_inv(d);
@@ -942,6 +998,22 @@ __device__ __forceinline__ bool trace_wide(const DevScene<float>& sc, const unsi
           break;
         }
         cur = pop();
+      } else if constexpr (W8) {  // a compressed 8-wide node (HBM trees)
+        uint32_t k[8];
+        uint4 c0, c1;
+        wide8_keys(sc.wnodes8 + cur, o, inv, tmin, tmax, k, c0, c1);
+        if (k[0] == 0xFFFFFFFFu) {
+          if (sp == 0) {
+            have = false;
+            break;
+          }
+          cur = pop();
+        } else {
+#pragma unroll
+          for (int j = 7; j >= 1; j--)
+            if (k[j] != 0xFFFFFFFFu) push(wide8_child(k[j], c0, c1));
+          cur = wide8_child(k[0], c0, c1);
+        }
       } else {
         const float4* nd = LDSN ? (const float4*)(lds_nodes + (cur << 4)) : (const float4*)(sc.wnodes + cur);
         const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];

@@ -58,6 +58,9 @@ constexpr int kBlock = 256;
 #ifndef RT_COLD_LDS  // the volume linear program: the cold path state in LDS (Path, LC)
 #define RT_COLD_LDS 1
 #endif
+#ifndef RT_F64_TAIL  // 1: fp64 renders use the fp32 item layout (bulk + tail items); 0: uniform items of 16
+#define RT_F64_TAIL 1
+#endif
 #ifndef RT_PERSIST_MODE  // 2: dynamic (per-XCD heads), 1: static striding (development A/B)
 #define RT_PERSIST_MODE 2
 #endif
@@ -192,6 +195,11 @@ __device__ __forceinline__ double* cold_doubles() {
   __shared__ double w[kColdDoubles * kBlock];
   return w + threadIdx.x;
 }
+// the fp64 item sum of an LC path ([component][lane]; fp32 keeps it in three of the cold words)
+__device__ __forceinline__ __attribute__((unused)) double* cold_acc64() {
+  __shared__ double w[3 * kBlock];
+  return w + threadIdx.x;
+}
 
 // One path's state. The fields a segment reads stay in registers; the cold ones -- the item's
 // running sum, its pixel and RNG key, the sample counter and range, the fp64 camera base -- are
@@ -214,11 +222,20 @@ struct Path {
   enum { kAcc = 0, kKa = 3, kItem, kSample, kSend, kXy };
   __device__ __forceinline__ static uint32_t& w(int k) { return cold_words()[k * kBlock]; }
   __device__ __forceinline__ V<R> acc() const {
-    if constexpr (LC) return mkv(__uint_as_float(w(kAcc)), __uint_as_float(w(kAcc + 1)), __uint_as_float(w(kAcc + 2)));
-    else return acc_;
+    if constexpr (LC && sizeof(R) == 8) {
+      return mkv(cold_acc64()[0], cold_acc64()[kBlock], cold_acc64()[2 * kBlock]);
+    } else if constexpr (LC) {
+      return mkv(__uint_as_float(w(kAcc)), __uint_as_float(w(kAcc + 1)), __uint_as_float(w(kAcc + 2)));
+    } else {
+      return acc_;
+    }
   }
   __device__ __forceinline__ void set_acc(V<R> v) {
-    if constexpr (LC) {
+    if constexpr (LC && sizeof(R) == 8) {
+      cold_acc64()[0] = v.x;
+      cold_acc64()[kBlock] = v.y;
+      cold_acc64()[2 * kBlock] = v.z;
+    } else if constexpr (LC) {
       w(kAcc) = __float_as_uint(v.x);
       w(kAcc + 1) = __float_as_uint(v.y);
       w(kAcc + 2) = __float_as_uint(v.z);
@@ -370,7 +387,7 @@ __device__ __forceinline__ void begin_item(const Params<R>& p, PS& s, uint32_t i
   const uint32_t xy = p.pixmap[item - chunk * p.npix];
   // fp64 items are uniform (the host never gives them a tail): compiled out, the select costs
   // the fp64 Cornell kernel 10 VGPRs, 3 -> 2 waves per SIMD (C2 f64 5.22 -> 4.08 Gsamples/s)
-  const bool bulk = sizeof(R) == 8 || chunk < p.k_bulk;
+  const bool bulk = (sizeof(R) == 8 && !RT_F64_TAIL) || chunk < p.k_bulk;
   const uint32_t first = bulk ? chunk * p.chunk : p.k_bulk * p.chunk + (chunk - p.k_bulk) * p.tail_chunk;
   s.set_item(item);
   s.set_sample(first);
@@ -752,6 +769,9 @@ struct LinearTrav {
 #ifndef RT_FLAT_WAVES
 #define RT_FLAT_WAVES 7
 #endif
+#ifndef RT_F64_COLD_LDS  // fp64 flat program: the cold path state (item sum, pixel, keys, camera base) in LDS
+#define RT_F64_COLD_LDS 1
+#endif
 #ifndef RT_FLAT_WAVES_F64  // fp64 flat program: waves per SIMD the register budget is cut for (1: none)
 #define RT_FLAT_WAVES_F64 4
 #endif
@@ -762,7 +782,8 @@ struct FlatTrav {
   static constexpr int kLdsNodes = 0;
   static constexpr bool kFlat = true;
   static constexpr bool kWide = false;
-  static constexpr bool kColdLds = false;  // fp32: 72 -> 64 VGPRs, but C2 23.5 -> 24.1 ms/frame
+  // fp32: 72 -> 64 VGPRs, but C2 23.5 -> 24.1 ms/frame; fp64: see RT_F64_COLD_LDS
+  static constexpr bool kColdLds = sizeof(R) == 8 && RT_F64_COLD_LDS;
   template <class PS>
   __device__ __forceinline__ static void run(const DevScene<R>& sc, const Node<R>*, const PS& s, Keys, uint32_t*,
                                              R& t, uint32_t& e, int32_t& i, uint32_t& nm) {
@@ -808,10 +829,10 @@ struct StackTrav {
 #ifndef RT_SHADE_BATCH  // < 64: a wave stops traversing to shade once this many of its lanes have finished
 #define RT_SHADE_BATCH 64  // (LDS-resident tree; measured on C3: 16 / 32 / 48 are 1-2 % slower than never pausing)
 #endif
-#ifndef RT_SHADE_BATCH_GLOBAL  // the same for trees in HBM (speculative traversal)
-#define RT_SHADE_BATCH_GLOBAL 64
+#ifndef RT_SHADE_BATCH_GLOBAL  // the same for trees in HBM (speculative traversal): C4 stand-in 413.6 ms/frame
+#define RT_SHADE_BATCH_GLOBAL 48  // never pausing, 415.2 / 370.8 / 363.8 / 362.5 / 368.4 / 379.6 at 16/32/40/48/56/60
 #endif
-template <bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN>
+template <bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN, bool W8 = false>
 struct WideTrav {
   static constexpr int kStack = 0;
   static constexpr int kLdsNodes = 0;
@@ -824,7 +845,9 @@ struct WideTrav {
   __host__ __device__ static uint32_t stack_offset(uint32_t n_wnodes, uint32_t n_words) {
     return LDSN ? n_wnodes * kWNodeLdsStride + n_words * 16u : 0u;
   }
-  __host__ __device__ static uint32_t root(const DevScene<float>& sc) { return LDSN ? wide_code16(sc.wroot) : sc.wroot; }
+  __host__ __device__ static uint32_t root(const DevScene<float>& sc) {
+    return W8 ? sc.wroot8 : (LDSN ? wide_code16(sc.wroot) : sc.wroot);
+  }
   __device__ __forceinline__ static StackT* fill(const DevScene<float>& sc, uint4* lds) {
     unsigned char* base = (unsigned char*)lds;
     if constexpr (LDSN) {
@@ -848,7 +871,7 @@ struct WideTrav {
   __device__ __forceinline__ static bool steps(const DevScene<float>& sc, const Node<float>* lds, const PS& s,
                                                StackT* stk, WideRay& ry) {
     const unsigned char* base = (const unsigned char*)lds;
-    return trace_wide<SPH, TRI, QUAD, MOV, LDSN, kBlock, LDSN ? RT_SHADE_BATCH : RT_SHADE_BATCH_GLOBAL>(
+    return trace_wide<SPH, TRI, QUAD, MOV, LDSN, kBlock, LDSN ? RT_SHADE_BATCH : RT_SHADE_BATCH_GLOBAL, W8>(
         sc, base, (const float4*)(base + sc.n_wnodes * kWNodeLdsStride), s.o, s.d, s.tm, s.xe, stk, ry);
   }
 };
@@ -1371,6 +1394,10 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
   s.wide_stack = h.wide_stack;
   s.wide_kinds = h.wide_kinds;
   s.wide_big = h.wide_big;
+  s.wnodes8 = (const WNode8*)at(h.off_wnodes8);
+  s.wroot8 = h.wroot8;
+  s.wide8_stack = h.wide8_stack;
+  s.has_wide8 = (int32_t)h.has_wide8;
   return s;
 }
 
@@ -1414,10 +1441,10 @@ void launch_one(KernelT kern, Params<R> p, uint32_t grid, hipStream_t st, size_t
 
 // Dynamic LDS of a wide-BVH launch: the whole tree when it fits the budget (LDSN), else the stack only.
 constexpr size_t kWideLdsBudget = 40u << 10;  // bytes per 256-lane block: 4 blocks per CU of 160 KiB
-inline size_t wide_lds_bytes(const DevScene<float>& sc, bool ldsn) {
+inline size_t wide_lds_bytes(const DevScene<float>& sc, bool ldsn, bool w8 = false) {
   // an LDS tree: every entry in LDS, uint16; a tree in HBM: up to kWideLdsStack uint32 entries (the rest spill)
   const size_t stack = ldsn ? (size_t)sc.wide_stack * kBlock * 2u
-                            : (size_t)std::min<uint32_t>(sc.wide_stack, kWideLdsStack) * kBlock * 4u;
+                            : (size_t)std::min<uint32_t>(w8 ? sc.wide8_stack : sc.wide_stack, kWideLdsStack) * kBlock * 4u;
   return (ldsn ? (size_t)sc.n_wnodes * kWNodeLdsStride + (size_t)sc.n_wprim_words * 16u : 0u) + stack;
 }
 template <bool SPH, bool TRI, bool QUAD, bool MOV>
@@ -1426,7 +1453,11 @@ void launch_wide_k(const Params<float>& p, uint32_t grid, hipStream_t st) {
   // LDS-resident trees use 16-bit child codes (wide_code16): node offset (index x 9) < 2^15, first word < 2^12
   if (full <= kWideLdsBudget && p.sc.n_wnodes * kWNodeLdsUnits < 0x8000u && p.sc.n_wprim_words <= 0x1000u)
     launch_one(k_persist_occ<float, WideTrav<SPH, TRI, QUAD, MOV, true>, false>, p, grid, st, full);
-  else  // the spill area holds spill_lanes lanes: never launch more (the resident grid is below it)
+  else if (p.sc.has_wide8)  // the compressed 8-wide tree (the spill area holds spill_lanes lanes: never launch more)
+    launch_one(k_persist_occ<float, WideTrav<SPH, TRI, QUAD, MOV, false, true>, false>, p,
+               p.sc.wide_spill ? std::min<uint32_t>(grid, p.sc.spill_lanes / kBlock) : grid, st,
+               wide_lds_bytes(p.sc, false, true));
+  else
     launch_one(k_persist_occ<float, WideTrav<SPH, TRI, QUAD, MOV, false>, false>, p,
                p.sc.wide_spill ? std::min<uint32_t>(grid, p.sc.spill_lanes / kBlock) : grid, st,
                wide_lds_bytes(p.sc, false));
@@ -1551,17 +1582,17 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     const uint32_t spp = (uint32_t)prm->spp;
     // the flat program's items are cheaper per sample, so its default items are twice as long
     // (fewer item ends, dequeues and partial-sum stores; C2: 23.9 -> 23.5 ms/frame)
-    const bool flat_prog = !f64 && hdr.has_flat && prm->traversal != RT_TRAV_ORDERED &&
+    const bool flat_prog = (!f64 || RT_F64_TAIL) && hdr.has_flat && prm->traversal != RT_TRAV_ORDERED &&
                            make_view(cam).mode == RT_CAM_PERSPECTIVE && !(hdr.n_texdata > 0 || hdr.has_cell_noise);
     const uint32_t chunk0 = prm->samples_per_item > 0 ? std::min<uint32_t>((uint32_t)prm->samples_per_item, spp)
-                                                     : std::min<uint32_t>(f64 ? kAutoChunk : auto_chunk(flat_prog), spp);
+                                                     : std::min<uint32_t>((f64 && !RT_F64_TAIL) ? kAutoChunk : auto_chunk(flat_prog), spp);
     // The frame's last items are short (auto item size only): a lane that takes a long item just
     // before the queue runs dry keeps its wave resident while the others idle, and a small frame
     // (one rank of eight) has few items per lane. The last tail_samples of every pixel come in
     // items of tail_chunk samples; both depend on spp alone, so the image is the same for any
     // tiling or rank count.
     uint32_t chunk = chunk0, tail_chunk = chunk0, k_bulk = (spp + chunk0 - 1) / chunk0, nchunks = k_bulk;
-    if (prm->samples_per_item <= 0 && !f64) {  // fp64: uniform items of 16 (C2 f64 with the fp32
+    if (prm->samples_per_item <= 0 && (!f64 || RT_F64_TAIL)) {  // fp64: uniform items of 16 (C2 f64 with the fp32
                                                 // layout: 5.22 -> 4.04 Gsamples/s)
       const uint32_t ts = std::min<uint32_t>(spp, (uint32_t)((double)spp * auto_tail_frac(flat_prog) + 0.5));
       tail_chunk = std::min(chunk, auto_tail_chunk(flat_prog));
@@ -1614,12 +1645,13 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     unsigned char* sp = (unsigned char*)c->state.ptr;
     Params<R> p{};
     p.sc = dev_scene<R>(hdr, sbase);
-    if (!f64 && hdr.has_wide && hdr.wide_stack > kWideLdsStack) {
+    const uint32_t wide_need = std::max(hdr.wide_stack, hdr.has_wide8 ? hdr.wide8_stack : 0u);
+    if (!f64 && hdr.has_wide && wide_need > kWideLdsStack) {
       // a deep wide tree: a spill area of (need - kWideLdsStack) entries for every lane the chip can hold
       int ncu = 0;
       RT_HIP(c, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
       const uint32_t lanes = (uint32_t)std::max(ncu, 1) * 2048u;  // 32 waves of 64 per CU at most
-      if ((s = ensure(c, c->wide_spill, 4ull * (hdr.wide_stack - kWideLdsStack) * lanes)) != RT_OK) return s;
+      if ((s = ensure(c, c->wide_spill, 4ull * (wide_need - kWideLdsStack) * lanes)) != RT_OK) return s;
       p.sc.wide_spill = (uint32_t*)c->wide_spill.ptr;
       p.sc.spill_lanes = lanes;
     }

@@ -207,6 +207,23 @@ struct alignas(16) WNode {
   uint32_t child[4];
   uint32_t pad[4];
 };
+// The compressed 8-wide node (round 3) for trees that stay in HBM (the C4 mesh): child boxes
+// quantised to 8 bits per plane against the node's origin with a power-of-two quantum per axis
+// (Ylitie, Karras & Laine 2017), so one node holds 8 children in 96 B where the 4-wide node needs
+// 128 B for 4, and a ray's path from the root has half the levels -- half the dependent fetches.
+//   child k's box on axis a: [o_a + qlo_a[k] s_a, o_a + qhi_a[k] s_a], s_a = 2^(e_a - 127);
+//   the builder rounds outward and pads one quantum on each side, so the box is conservative.
+//   qlo / qhi: for axis a, words 2a and 2a + 1 hold the bytes of slots 0-3 and 4-7.
+//   meta: bytes 0-2 e_x, e_y, e_z; byte 3 the children in use (slots 0..n-1).
+//   child[k]: as WNode (an inner node's index in the 8-wide array, or a leaf code).
+struct alignas(16) WNode8 {
+  float ox, oy, oz;
+  uint32_t meta;
+  uint32_t qlo[6];
+  uint32_t qhi[6];
+  uint32_t child[8];
+};
+static_assert(sizeof(WNode8) == 96, "WNode8 is six 16-byte loads");
 constexpr uint32_t kWLeaf = 0x80000000u;
 constexpr uint32_t kWCountShift = 25;  // leaf: up to 64 primitives, first word < 2^25
 constexpr uint32_t kWFirstMask = (1u << kWCountShift) - 1u;
@@ -289,7 +306,12 @@ struct SceneHeader {
   uint32_t wide_kinds;   // WK_* bits
   uint32_t has_wide;
   uint32_t wide_big;     // primitives at the head of the word stream tested before the tree (huge boxes)
-  uint32_t wide_pad_[3];
+  uint32_t wroot8;       // the 8-wide tree over the same leaves (has_wide8): root code
+  uint32_t wide8_stack;  // its stack need
+  uint32_t has_wide8;
+  uint64_t off_wnodes8;
+  uint32_t n_wnodes8;
+  uint32_t wide8_pad_;
 };
 
 }  // namespace rtd

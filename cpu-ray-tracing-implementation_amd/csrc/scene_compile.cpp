@@ -1171,24 +1171,27 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
   };
   for (const Item& it : big)
     if (!put_prim(it.entry)) return false;
-  auto leaf_code = [&](const BN& nd, uint32_t& code) {
+  // a leaf's words are emitted once; the 8-wide tree below refers to the same words
+  std::vector<int64_t> leaf_memo(bn.size(), -1);
+  auto leaf_code = [&](int b, uint32_t& code) {
+    if (leaf_memo[(size_t)b] >= 0) {
+      code = (uint32_t)leaf_memo[(size_t)b];
+      return true;
+    }
+    const BN& nd = bn[(size_t)b];
     const size_t first = words.size();
     if (nd.count == 0 || nd.count > 64 || first > kWFirstMask) return false;
     for (size_t i = nd.first; i < nd.first + nd.count; i++)
       if (!put_prim(prims[order[i]].entry)) return false;
     code = kWLeaf | (uint32_t)(nd.count - 1) << kWCountShift | (uint32_t)first;
+    leaf_memo[(size_t)b] = code;
     return true;
   };
-  std::vector<WNode> wn;
-  // collapse: node of binary node `b` -> its index; stack need returned through `need`
-  std::function<bool(int, uint32_t&, int&)> emit = [&](int b, uint32_t& code, int& need) -> bool {
+  // the children of binary node b in a `width`-wide node: open the child of largest area until full
+  auto collapse = [&](int b, size_t width) {
     const BN& nd = bn[(size_t)b];
-    if (nd.left < 0) {
-      need = 0;
-      return leaf_code(nd, code);
-    }
     std::vector<int> ch{nd.left, nd.right};
-    while (ch.size() < 4) {
+    while (ch.size() < width) {
       int pick = -1;
       double best = -1;
       for (size_t k = 0; k < ch.size(); k++) {
@@ -1204,6 +1207,17 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
       ch[(size_t)pick] = l;
       ch.insert(ch.begin() + pick + 1, r);
     }
+    return ch;
+  };
+  std::vector<WNode> wn;
+  // collapse: node of binary node `b` -> its index; stack need returned through `need`
+  std::function<bool(int, uint32_t&, int&)> emit = [&](int b, uint32_t& code, int& need) -> bool {
+    const BN& nd = bn[(size_t)b];
+    if (nd.left < 0) {
+      need = 0;
+      return leaf_code(b, code);
+    }
+    const std::vector<int> ch = collapse(b, 4);
     const size_t idx = wn.size();
     if (idx >= kWLeaf) return false;
     wn.emplace_back();
@@ -1240,6 +1254,76 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
     std::fprintf(stderr, "[wide] ok %d need %d nodes %zu words %zu binary nodes %zu\n", (int)ok, need, wn.size(),
                  words.size(), bn.size());
   if (!ok || need > kWideStackMax) return false;
+
+  // The compressed 8-wide tree (rt_scene.h WNode8) over the same leaves, for the kernels that keep
+  // the tree in HBM. Quantisation per node: origin = the node box's low corner rounded down to
+  // float, quantum s_a = the power of two with (hi_a - o_a) / s_a <= 253, child planes rounded
+  // outward (the kernel's rounding of plane distances is covered by the slab test's relative
+  // widening, box_slack, as for the float boxes of the 4-wide nodes).
+  std::vector<WNode8> wn8;
+  const double kPad8 = std::getenv("RT_DEV_WIDE8_PAD") ? std::atof(std::getenv("RT_DEV_WIDE8_PAD")) : 0.0;
+  std::function<bool(int, uint32_t&, int&)> emit8 = [&](int b, uint32_t& code, int& need8) -> bool {
+    const BN& nd = bn[(size_t)b];
+    if (nd.left < 0) {
+      need8 = 0;
+      return leaf_code(b, code);
+    }
+    const std::vector<int> ch = collapse(b, 8);
+    const size_t idx = wn8.size();
+    if (idx >= kWLeaf) return false;
+    wn8.emplace_back();
+    Box nb;
+    for (int c : ch) nb.grow(bn[(size_t)c].box);
+    float o[3];
+    int ex[3];
+    double sc[3];
+    for (int a = 0; a < 3; a++) {
+      o[a] = down(nb.lo[a]);
+      const double ext = nb.hi[a] - (double)o[a];
+      int e = -100;
+      if (ext > 0) e = std::max(-126, (int)std::ceil(std::log2(ext / 253.0)));
+      while (std::ldexp(253.0, e) < ext) e++;
+      if (e > 127) return false;
+      ex[a] = e;
+      sc[a] = std::ldexp(1.0, e);
+    }
+    WNode8 w{};
+    w.ox = o[0];
+    w.oy = o[1];
+    w.oz = o[2];
+    w.meta = (uint32_t)(ex[0] + 127) | (uint32_t)(ex[1] + 127) << 8 | (uint32_t)(ex[2] + 127) << 16 |
+             (uint32_t)ch.size() << 24;
+    int sub = 0;
+    for (size_t c = 0; c < ch.size(); c++) {
+      const Box& bx = bn[(size_t)ch[c]].box;
+      for (int a = 0; a < 3; a++) {
+        const double lo = std::floor((bx.lo[a] - (double)o[a]) / sc[a]) - kPad8;
+        const double hi = std::ceil((bx.hi[a] - (double)o[a]) / sc[a]) + kPad8;
+        const uint32_t ql = (uint32_t)std::min(255.0, std::max(0.0, lo));
+        const uint32_t qh = (uint32_t)std::min(255.0, std::max(0.0, hi));
+        w.qlo[2 * a + c / 4] |= ql << (8 * (c % 4));
+        w.qhi[2 * a + c / 4] |= qh << (8 * (c % 4));
+      }
+    }
+    wn8[idx] = w;
+    for (size_t c = 0; c < ch.size(); c++) {
+      uint32_t cc;
+      int cn;
+      if (!emit8(ch[c], cc, cn)) return false;
+      sub = std::max(sub, cn);
+      wn8[idx].child[c] = cc;
+    }
+    need8 = (int)ch.size() - 1 + sub;
+    code = (uint32_t)idx;
+    return true;
+  };
+  uint32_t root8 = 0;
+  int need8 = 0;
+  // measured slower than the 4-wide tree on the C4 stand-in (507 vs 364 ms/frame: the 8 dequantised
+  // slab tests and the 19-comparator sort cost more VALU than the halved fetch depth saves), so it is
+  // built only on request (RT_DEV_WIDE8=1, development A/B)
+  const char* w8 = std::getenv("RT_DEV_WIDE8");
+  const bool ok8 = w8 && *w8 == '1' && emit8(0, root8, need8) && need8 <= kWideStackMax;
   SceneHeader& h = out->hdr;
   h.off_wnodes = append(out->blob32, wn);
   h.off_wprims = append(out->blob32, words);
@@ -1252,6 +1336,15 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
   h.wide_kinds = kinds;
   h.wide_big = (uint32_t)big.size();
   h.has_wide = 1;
+  if (ok8) {
+    h.off_wnodes8 = append(out->blob32, wn8);
+    out->blob32.resize((out->blob32.size() + 255) & ~size_t(255));
+    h.bytes = out->blob32.size();
+    h.n_wnodes8 = (uint32_t)wn8.size();
+    h.wroot8 = root8;
+    h.wide8_stack = (uint32_t)std::max(1, need8);
+    h.has_wide8 = 1;
+  }
   return true;
 }
 

@@ -137,3 +137,16 @@ def test_pixel_map_follows_the_last_tiles_height(ctx):
     ctx.render(cam, 2, 5, seed=4, precision=F32, tiles=[(0, 0, W, H // 2)])  # rewrites the first half only
     again = ctx.render(cam, 2, 5, seed=4, precision=F32, tiles=[(0, 0, W, H)])  # same entry as the last list
     assert np.array_equal(again.reshape(fresh.shape), fresh)
+
+
+def test_compressed_wide8_mesh_matches_binary(ctx, tmp_path, monkeypatch):
+    # the opt-in compressed 8-wide tree (rt_scene.h WNode8, RT_DEV_WIDE8=1 at scene compile): quantised
+    # child boxes must stay conservative, so the closest hits equal the binary BVH's (ties aside)
+    from rt_amd import synth_gltf
+    monkeypatch.setenv("RT_SPONZA_GLTF", synth_gltf.write_sponza_standin(str(tmp_path)))
+    monkeypatch.setenv("RT_DEV_WIDE8", "1")
+    cs = plugin.ConfigScene("sponza", 64, 16.0 / 9.0)
+    wide, binary = both_traversals(ctx, cs.desc, cs.cam, 4, 5, 3)
+    differ = np.abs(wide - binary).max(-1) > 0
+    assert differ.mean() < 5e-3, int(differ.sum())
+    assert (rmse(wide, binary) < 1e-4).all(), rmse(wide, binary)
