@@ -289,9 +289,8 @@ struct DevScene {
   uint32_t n_wnodes, n_wprim_words, wroot, wide_stack, wide_kinds;
   int32_t has_wide;
   uint32_t wide_big;  // primitives at the head of the word stream, tested before the tree
-  const WNode8* wnodes8;  // the compressed 8-wide tree over the same leaves (has_wide8)
-  uint32_t wroot8, wide8_stack;
-  int32_t has_wide8;
+  const void* wnodesq;  // the quantised tree over the same leaves (WNodeQ4 / WNode8 by wideq_width; 0: none)
+  uint32_t wrootq, wideq_stack, wideq_width;
   // a tree in HBM keeps at most kWideLdsStack stack entries per lane in LDS; deeper entries (rare:
   // every child of every node on a path hit) go to wide_spill[(depth - kWideLdsStack) * spill_lanes + lane]
   uint32_t* wide_spill;
@@ -898,17 +897,43 @@ __device__ __forceinline__ void wide8_keys(const WNode8* node, V<float> o, V<flo
   RT_CS8(1, 2) RT_CS8(3, 4) RT_CS8(5, 6)
 #undef RT_CS8
 }
+// the same for the four children of a quantised 4-wide node (rt_scene.h WNodeQ4), sorted by the
+// 5-comparator network of the float nodes
+__device__ __forceinline__ void wideq4_keys(const WNodeQ4* node, V<float> o, V<float> inv, float tmin, float tmax,
+                                            uint32_t& k0, uint32_t& k1, uint32_t& k2, uint32_t& k3, uint4& cc) {
+  const uint4* nd = (const uint4*)node;
+  const uint4 h = nd[0], qa = nd[1], qb = nd[2];  // qa: qlo x, y, z, qhi x; qb: qhi y, z
+  cc = nd[3];
+  const float ax = __uint_as_float((h.w & 0xFFu) << 23) * inv.x, bx = (__uint_as_float(h.x) - o.x) * inv.x;
+  const float ay = __uint_as_float(((h.w >> 8) & 0xFFu) << 23) * inv.y, by = (__uint_as_float(h.y) - o.y) * inv.y;
+  const float az = __uint_as_float(((h.w >> 16) & 0xFFu) << 23) * inv.z, bz = (__uint_as_float(h.z) - o.z) * inv.z;
+  const uint32_t n = h.w >> 24;
+  uint32_t k[4];
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const int sh = 8 * c;
+    auto q = [&](uint32_t w) { return (float)((w >> sh) & 0xFFu); };
+    const float tx0 = fmaf(q(qa.x), ax, bx), tx1 = fmaf(q(qa.w), ax, bx);
+    const float ty0 = fmaf(q(qa.y), ay, by), ty1 = fmaf(q(qb.x), ay, by);
+    const float tz0 = fmaf(q(qa.z), az, bz), tz1 = fmaf(q(qb.y), az, bz);
+    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
+    const float tf =
+        fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax)) * Num<float>::box_slack();
+    k[c] = ((uint32_t)c < n && tn <= tf) ? ((__float_as_uint(tn) & ~3u) | (uint32_t)c) : 0xFFFFFFFFu;
+  }
+  k0 = k[0], k1 = k[1], k2 = k[2], k3 = k[3];
+}
 // the child code in slot (key & 7) of the node whose codes are c0 (slots 0-3) and c1 (4-7)
 __device__ __forceinline__ uint32_t wide8_child(uint32_t key, const uint4& c0, const uint4& c1) {
   const uint4 c = (key & 4u) ? c1 : c0;
   const uint32_t lo = (key & 1u) ? c.y : c.x, hi = (key & 1u) ? c.w : c.z;
   return (key & 2u) ? hi : lo;
 }
-template <bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN, int BLOCK, int PAUSE, bool W8 = false>
+template <bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN, int BLOCK, int PAUSE, int QN = 0>
 __device__ __forceinline__ bool trace_wide(const DevScene<float>& sc, const unsigned char* lds_nodes,
                                            const float4* lds_prims, V<float> o, V<float> d, float time,
                                            uint32_t excl_e, WStackT<LDSN>* stk, WideRay& ry) {
-  static_assert(!W8 || (!LDSN && RT_WIDE_SPEC), "the 8-wide nodes are traversed speculatively, from HBM");
+  static_assert(QN == 0 || (!LDSN && RT_WIDE_SPEC), "quantised nodes are traversed speculatively, from HBM");
   constexpr uint32_t kLeafBit = LDSN ? kWLeaf16 : kWLeaf;
   const float tmin = 0.001f;
   const V<float> inv = box_inv(d);
@@ -998,10 +1023,10 @@ __device__ __forceinline__ bool trace_wide(const DevScene<float>& sc, const unsi
           break;
         }
         cur = pop();
-      } else if constexpr (W8) {  // a compressed 8-wide node (HBM trees)
+      } else if constexpr (QN == 8) {  // a compressed 8-wide node (HBM trees)
         uint32_t k[8];
         uint4 c0, c1;
-        wide8_keys(sc.wnodes8 + cur, o, inv, tmin, tmax, k, c0, c1);
+        wide8_keys((const WNode8*)sc.wnodesq + cur, o, inv, tmin, tmax, k, c0, c1);
         if (k[0] == 0xFFFFFFFFu) {
           if (sp == 0) {
             have = false;
@@ -1016,9 +1041,18 @@ __device__ __forceinline__ bool trace_wide(const DevScene<float>& sc, const unsi
         }
       } else {
         const float4* nd = LDSN ? (const float4*)(lds_nodes + (cur << 4)) : (const float4*)(sc.wnodes + cur);
-        const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
         uint4 cc{};
-        if constexpr (!LDSN) cc = *(const uint4*)(nd + 6);
+        uint32_t k0, k1, k2, k3;
+        if constexpr (QN == 4) {  // a quantised 4-wide node (HBM trees)
+          wideq4_keys((const WNodeQ4*)sc.wnodesq + cur, o, inv, tmin, tmax, k0, k1, k2, k3, cc);
+        } else {
+          const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
+          if constexpr (!LDSN) cc = *(const uint4*)(nd + 6);
+          k0 = slab(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, 0u);
+          k1 = slab(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, 1u);
+          k2 = slab(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, 2u);
+          k3 = slab(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, 3u);
+        }
         auto child = [&](uint32_t k) -> uint32_t {
           if constexpr (LDSN) {
             return ((const uint16_t*)(nd + 6))[k & 3u];
@@ -1027,10 +1061,6 @@ __device__ __forceinline__ bool trace_wide(const DevScene<float>& sc, const unsi
             return sl == 0 ? cc.x : (sl == 1 ? cc.y : (sl == 2 ? cc.z : cc.w));
           }
         };
-        uint32_t k0 = slab(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, 0u);
-        uint32_t k1 = slab(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, 1u);
-        uint32_t k2 = slab(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, 2u);
-        uint32_t k3 = slab(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, 3u);
 #define RT_CS(a, b)                 \
   {                                 \
     const uint32_t lo_ = min(a, b); \

@@ -832,7 +832,7 @@ struct StackTrav {
 #ifndef RT_SHADE_BATCH_GLOBAL  // the same for trees in HBM (speculative traversal): C4 stand-in 413.6 ms/frame
 #define RT_SHADE_BATCH_GLOBAL 48  // never pausing, 415.2 / 370.8 / 363.8 / 362.5 / 368.4 / 379.6 at 16/32/40/48/56/60
 #endif
-template <bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN, bool W8 = false>
+template <bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN, int QN = 0>
 struct WideTrav {
   static constexpr int kStack = 0;
   static constexpr int kLdsNodes = 0;
@@ -846,7 +846,7 @@ struct WideTrav {
     return LDSN ? n_wnodes * kWNodeLdsStride + n_words * 16u : 0u;
   }
   __host__ __device__ static uint32_t root(const DevScene<float>& sc) {
-    return W8 ? sc.wroot8 : (LDSN ? wide_code16(sc.wroot) : sc.wroot);
+    return QN ? sc.wrootq : (LDSN ? wide_code16(sc.wroot) : sc.wroot);
   }
   __device__ __forceinline__ static StackT* fill(const DevScene<float>& sc, uint4* lds) {
     unsigned char* base = (unsigned char*)lds;
@@ -871,7 +871,7 @@ struct WideTrav {
   __device__ __forceinline__ static bool steps(const DevScene<float>& sc, const Node<float>* lds, const PS& s,
                                                StackT* stk, WideRay& ry) {
     const unsigned char* base = (const unsigned char*)lds;
-    return trace_wide<SPH, TRI, QUAD, MOV, LDSN, kBlock, LDSN ? RT_SHADE_BATCH : RT_SHADE_BATCH_GLOBAL, W8>(
+    return trace_wide<SPH, TRI, QUAD, MOV, LDSN, kBlock, LDSN ? RT_SHADE_BATCH : RT_SHADE_BATCH_GLOBAL, QN>(
         sc, base, (const float4*)(base + sc.n_wnodes * kWNodeLdsStride), s.o, s.d, s.tm, s.xe, stk, ry);
   }
 };
@@ -1394,10 +1394,10 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
   s.wide_stack = h.wide_stack;
   s.wide_kinds = h.wide_kinds;
   s.wide_big = h.wide_big;
-  s.wnodes8 = (const WNode8*)at(h.off_wnodes8);
-  s.wroot8 = h.wroot8;
-  s.wide8_stack = h.wide8_stack;
-  s.has_wide8 = (int32_t)h.has_wide8;
+  s.wnodesq = at(h.off_wnodesq);
+  s.wrootq = h.wrootq;
+  s.wideq_stack = h.wideq_stack;
+  s.wideq_width = h.wideq_width;
   return s;
 }
 
@@ -1444,7 +1444,7 @@ constexpr size_t kWideLdsBudget = 40u << 10;  // bytes per 256-lane block: 4 blo
 inline size_t wide_lds_bytes(const DevScene<float>& sc, bool ldsn, bool w8 = false) {
   // an LDS tree: every entry in LDS, uint16; a tree in HBM: up to kWideLdsStack uint32 entries (the rest spill)
   const size_t stack = ldsn ? (size_t)sc.wide_stack * kBlock * 2u
-                            : (size_t)std::min<uint32_t>(w8 ? sc.wide8_stack : sc.wide_stack, kWideLdsStack) * kBlock * 4u;
+                            : (size_t)std::min<uint32_t>(w8 ? sc.wideq_stack : sc.wide_stack, kWideLdsStack) * kBlock * 4u;
   return (ldsn ? (size_t)sc.n_wnodes * kWNodeLdsStride + (size_t)sc.n_wprim_words * 16u : 0u) + stack;
 }
 template <bool SPH, bool TRI, bool QUAD, bool MOV>
@@ -1453,8 +1453,12 @@ void launch_wide_k(const Params<float>& p, uint32_t grid, hipStream_t st) {
   // LDS-resident trees use 16-bit child codes (wide_code16): node offset (index x 9) < 2^15, first word < 2^12
   if (full <= kWideLdsBudget && p.sc.n_wnodes * kWNodeLdsUnits < 0x8000u && p.sc.n_wprim_words <= 0x1000u)
     launch_one(k_persist_occ<float, WideTrav<SPH, TRI, QUAD, MOV, true>, false>, p, grid, st, full);
-  else if (p.sc.has_wide8)  // the compressed 8-wide tree (the spill area holds spill_lanes lanes: never launch more)
-    launch_one(k_persist_occ<float, WideTrav<SPH, TRI, QUAD, MOV, false, true>, false>, p,
+  else if (p.sc.wideq_width == 4)  // the quantised tree (the spill area holds spill_lanes lanes: never launch more)
+    launch_one(k_persist_occ<float, WideTrav<SPH, TRI, QUAD, MOV, false, 4>, false>, p,
+               p.sc.wide_spill ? std::min<uint32_t>(grid, p.sc.spill_lanes / kBlock) : grid, st,
+               wide_lds_bytes(p.sc, false, true));
+  else if (p.sc.wideq_width == 8)
+    launch_one(k_persist_occ<float, WideTrav<SPH, TRI, QUAD, MOV, false, 8>, false>, p,
                p.sc.wide_spill ? std::min<uint32_t>(grid, p.sc.spill_lanes / kBlock) : grid, st,
                wide_lds_bytes(p.sc, false, true));
   else
@@ -1645,7 +1649,7 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     unsigned char* sp = (unsigned char*)c->state.ptr;
     Params<R> p{};
     p.sc = dev_scene<R>(hdr, sbase);
-    const uint32_t wide_need = std::max(hdr.wide_stack, hdr.has_wide8 ? hdr.wide8_stack : 0u);
+    const uint32_t wide_need = std::max(hdr.wide_stack, hdr.wideq_width ? hdr.wideq_stack : 0u);
     if (!f64 && hdr.has_wide && wide_need > kWideLdsStack) {
       // a deep wide tree: a spill area of (need - kWideLdsStack) entries for every lane the chip can hold
       int ncu = 0;

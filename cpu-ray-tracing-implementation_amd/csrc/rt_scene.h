@@ -207,7 +207,7 @@ struct alignas(16) WNode {
   uint32_t child[4];
   uint32_t pad[4];
 };
-// The compressed 8-wide node (round 3) for trees that stay in HBM (the C4 mesh): child boxes
+// The compressed 8-wide node (round 3; opt-in, RT_DEV_WIDEQ=8) for trees that stay in HBM: child boxes
 // quantised to 8 bits per plane against the node's origin with a power-of-two quantum per axis
 // (Ylitie, Karras & Laine 2017), so one node holds 8 children in 96 B where the 4-wide node needs
 // 128 B for 4, and a ray's path from the root has half the levels -- half the dependent fetches.
@@ -224,10 +224,23 @@ struct alignas(16) WNode8 {
   uint32_t child[8];
 };
 static_assert(sizeof(WNode8) == 96, "WNode8 is six 16-byte loads");
+// The quantised 4-wide node (round 3; opt-in, RT_DEV_WIDEQ=4): WNode's four children with WNode8's
+// quantised boxes in 64 B instead of 128 -- the C4 stand-in's 42,902 nodes fit in 2.7 MB, under one
+// XCD's 4 MB L2 -- measured slower than the float node there (scene_compile.cpp wide_bvh).
+// qlo[a] / qhi[a]: byte c = child c's plane on axis a.
+struct alignas(16) WNodeQ4 {
+  float ox, oy, oz;
+  uint32_t meta;
+  uint32_t qlo[3];
+  uint32_t qhi[3];
+  uint32_t pad[2];
+  uint32_t child[4];
+};
+static_assert(sizeof(WNodeQ4) == 64, "WNodeQ4 is four 16-byte loads");
 constexpr uint32_t kWLeaf = 0x80000000u;
 constexpr uint32_t kWCountShift = 25;  // leaf: up to 64 primitives, first word < 2^25
 constexpr uint32_t kWFirstMask = (1u << kWCountShift) - 1u;
-constexpr int kWLeafMax = 4;         // primitives per leaf (triangles, mixed kinds)
+constexpr int kWLeafMax = 3;         // primitives per leaf (triangles, mixed kinds)
 constexpr int kWLeafMaxSpheres = 6;  // sphere-only trees (at most 8: the LDS code's 3-bit count)
 constexpr int kWideStackMax = 96;  // stack entries a ray may need in the wide tree (beyond LDS: a spill area)
 // primitive kinds present (SceneHeader::wide_kinds)
@@ -306,12 +319,12 @@ struct SceneHeader {
   uint32_t wide_kinds;   // WK_* bits
   uint32_t has_wide;
   uint32_t wide_big;     // primitives at the head of the word stream tested before the tree (huge boxes)
-  uint32_t wroot8;       // the 8-wide tree over the same leaves (has_wide8): root code
-  uint32_t wide8_stack;  // its stack need
-  uint32_t has_wide8;
-  uint64_t off_wnodes8;
-  uint32_t n_wnodes8;
-  uint32_t wide8_pad_;
+  uint32_t wrootq;       // the quantised tree over the same leaves (wideq_width 4 or 8; 0: none): root code
+  uint32_t wideq_stack;  // its stack need
+  uint32_t wideq_width;
+  uint64_t off_wnodesq;
+  uint32_t n_wnodesq;
+  uint32_t wideq_pad_;
 };
 
 }  // namespace rtd

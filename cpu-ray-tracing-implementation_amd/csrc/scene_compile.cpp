@@ -1041,7 +1041,7 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
   // (node cost 1-8 primitive tests) was no better than the fixed sizes.
   bool all_spheres = true;
   for (const Item& it : prims) all_spheres = all_spheres && etype(it.entry) == E_SPHERE;
-  size_t leaf_max = (size_t)(all_spheres ? kWLeafMaxSpheres : kWLeafMax);
+  size_t leaf_max = (size_t)(all_spheres ? kWLeafMaxSpheres : kWLeafMax);  // triangles: 3 (r03j C4 357.9 vs 362.7)
   if (const char* v = std::getenv("RT_DEV_WIDE_LEAF")) leaf_max = (size_t)std::max(1, std::min(8, std::atoi(v)));
   // split planes: binned SAH over all three axes (C4's triangles: 743 -> 458 ms/frame against the
   // largest centroid extent only), but the largest axis only for sphere trees (C3: 64.2 vs 65.1)
@@ -1260,26 +1260,38 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
   // float, quantum s_a = the power of two with (hi_a - o_a) / s_a <= 253, child planes rounded
   // outward (the kernel's rounding of plane distances is covered by the slab test's relative
   // widening, box_slack, as for the float boxes of the 4-wide nodes).
-  std::vector<WNode8> wn8;
-  const double kPad8 = std::getenv("RT_DEV_WIDE8_PAD") ? std::atof(std::getenv("RT_DEV_WIDE8_PAD")) : 0.0;
-  std::function<bool(int, uint32_t&, int&)> emit8 = [&](int b, uint32_t& code, int& need8) -> bool {
+  // A quantised tree over the same leaves (rt_scene.h WNodeQ4 / WNode8), for the kernels that keep
+  // the tree in HBM. Quantisation per node: origin = the node box's low corner rounded down to
+  // float, quantum s_a = the power of two with (hi_a - o_a) / s_a <= 253, child planes rounded
+  // outward (the kernel's rounding of plane distances is covered by the slab test's relative
+  // widening, box_slack, as for the float boxes of the 4-wide nodes).
+  struct QN {
+    float o[3];
+    uint32_t meta;
+    uint32_t qlo[3][8], qhi[3][8];
+    uint32_t child[8];
+  };
+  std::vector<QN> qn;
+  const char* wq_env = std::getenv("RT_DEV_WIDEQ");
+  const int qwidth = wq_env ? std::atoi(wq_env) : 0;
+  std::function<bool(int, uint32_t&, int&)> emitq = [&](int b, uint32_t& code, int& needq) -> bool {
     const BN& nd = bn[(size_t)b];
     if (nd.left < 0) {
-      need8 = 0;
+      needq = 0;
       return leaf_code(b, code);
     }
-    const std::vector<int> ch = collapse(b, 8);
-    const size_t idx = wn8.size();
+    const std::vector<int> ch = collapse(b, (size_t)qwidth);
+    const size_t idx = qn.size();
     if (idx >= kWLeaf) return false;
-    wn8.emplace_back();
+    qn.emplace_back();
     Box nb;
     for (int c : ch) nb.grow(bn[(size_t)c].box);
-    float o[3];
-    int ex[3];
+    QN w{};
     double sc[3];
+    int ex[3];
     for (int a = 0; a < 3; a++) {
-      o[a] = down(nb.lo[a]);
-      const double ext = nb.hi[a] - (double)o[a];
+      w.o[a] = down(nb.lo[a]);
+      const double ext = nb.hi[a] - (double)w.o[a];
       int e = -100;
       if (ext > 0) e = std::max(-126, (int)std::ceil(std::log2(ext / 253.0)));
       while (std::ldexp(253.0, e) < ext) e++;
@@ -1287,44 +1299,38 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
       ex[a] = e;
       sc[a] = std::ldexp(1.0, e);
     }
-    WNode8 w{};
-    w.ox = o[0];
-    w.oy = o[1];
-    w.oz = o[2];
     w.meta = (uint32_t)(ex[0] + 127) | (uint32_t)(ex[1] + 127) << 8 | (uint32_t)(ex[2] + 127) << 16 |
              (uint32_t)ch.size() << 24;
-    int sub = 0;
     for (size_t c = 0; c < ch.size(); c++) {
       const Box& bx = bn[(size_t)ch[c]].box;
       for (int a = 0; a < 3; a++) {
-        const double lo = std::floor((bx.lo[a] - (double)o[a]) / sc[a]) - kPad8;
-        const double hi = std::ceil((bx.hi[a] - (double)o[a]) / sc[a]) + kPad8;
-        const uint32_t ql = (uint32_t)std::min(255.0, std::max(0.0, lo));
-        const uint32_t qh = (uint32_t)std::min(255.0, std::max(0.0, hi));
-        w.qlo[2 * a + c / 4] |= ql << (8 * (c % 4));
-        w.qhi[2 * a + c / 4] |= qh << (8 * (c % 4));
+        const double lo = std::floor((bx.lo[a] - (double)w.o[a]) / sc[a]);
+        const double hi = std::ceil((bx.hi[a] - (double)w.o[a]) / sc[a]);
+        w.qlo[a][c] = (uint32_t)std::min(255.0, std::max(0.0, lo));
+        w.qhi[a][c] = (uint32_t)std::min(255.0, std::max(0.0, hi));
       }
     }
-    wn8[idx] = w;
+    int sub = 0;
     for (size_t c = 0; c < ch.size(); c++) {
       uint32_t cc;
       int cn;
-      if (!emit8(ch[c], cc, cn)) return false;
+      if (!emitq(ch[c], cc, cn)) return false;
       sub = std::max(sub, cn);
-      wn8[idx].child[c] = cc;
+      w.child[c] = cc;
     }
-    need8 = (int)ch.size() - 1 + sub;
+    qn[idx] = w;
+    needq = (int)ch.size() - 1 + sub;
     code = (uint32_t)idx;
     return true;
   };
-  uint32_t root8 = 0;
-  int need8 = 0;
-  // measured slower than the 4-wide tree on the C4 stand-in (507 vs 364 ms/frame: the 8 dequantised
-  // slab tests and the 19-comparator sort cost more VALU than the halved fetch depth saves), so it is
-  // built only on request (RT_DEV_WIDE8=1, development A/B)
-  const char* w8 = std::getenv("RT_DEV_WIDE8");
-  const bool ok8 = w8 && *w8 == '1' && emit8(0, root8, need8) && need8 <= kWideStackMax;
-  SceneHeader& h = out->hdr;
+  uint32_t rootq = 0;
+  int needq = 0;
+  // RT_DEV_WIDEQ (development A/B; default 0: none, the float 4-wide tree serves HBM too): 4 the
+  // quantised 4-wide tree, 8 the compressed 8-wide one. Both measured slower on the C4 stand-in
+  // (r03j, ms/frame: float 4-wide 362.7, quantised 4-wide 386.5, 8-wide 506.0): the kernel there is
+  // bound by VALU issue in traversal, and dequantising the planes (and for 8-wide, a 19-comparator
+  // sort per visit) costs more than the smaller nodes and the halved fetch depth save.
+  const bool okq = (qwidth == 4 || qwidth == 8) && emitq(0, rootq, needq) && needq <= kWideStackMax;  SceneHeader& h = out->hdr;
   h.off_wnodes = append(out->blob32, wn);
   h.off_wprims = append(out->blob32, words);
   out->blob32.resize((out->blob32.size() + 255) & ~size_t(255));
@@ -1336,14 +1342,40 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
   h.wide_kinds = kinds;
   h.wide_big = (uint32_t)big.size();
   h.has_wide = 1;
-  if (ok8) {
-    h.off_wnodes8 = append(out->blob32, wn8);
+  if (okq) {
+    if (qwidth == 8) {
+      std::vector<WNode8> v(qn.size());
+      for (size_t i = 0; i < qn.size(); i++) {
+        WNode8& w = v[i];
+        w.ox = qn[i].o[0], w.oy = qn[i].o[1], w.oz = qn[i].o[2], w.meta = qn[i].meta;
+        for (int a = 0; a < 3; a++)
+          for (int c = 0; c < 8; c++) {
+            w.qlo[2 * a + c / 4] |= qn[i].qlo[a][c] << (8 * (c % 4));
+            w.qhi[2 * a + c / 4] |= qn[i].qhi[a][c] << (8 * (c % 4));
+          }
+        for (int c = 0; c < 8; c++) w.child[c] = qn[i].child[c];
+      }
+      h.off_wnodesq = append(out->blob32, v);
+    } else {
+      std::vector<WNodeQ4> v(qn.size());
+      for (size_t i = 0; i < qn.size(); i++) {
+        WNodeQ4& w = v[i];
+        w.ox = qn[i].o[0], w.oy = qn[i].o[1], w.oz = qn[i].o[2], w.meta = qn[i].meta;
+        for (int a = 0; a < 3; a++)
+          for (int c = 0; c < 4; c++) {
+            w.qlo[a] |= qn[i].qlo[a][c] << (8 * c);
+            w.qhi[a] |= qn[i].qhi[a][c] << (8 * c);
+          }
+        for (int c = 0; c < 4; c++) w.child[c] = qn[i].child[c];
+      }
+      h.off_wnodesq = append(out->blob32, v);
+    }
     out->blob32.resize((out->blob32.size() + 255) & ~size_t(255));
     h.bytes = out->blob32.size();
-    h.n_wnodes8 = (uint32_t)wn8.size();
-    h.wroot8 = root8;
-    h.wide8_stack = (uint32_t)std::max(1, need8);
-    h.has_wide8 = 1;
+    h.n_wnodesq = (uint32_t)qn.size();
+    h.wrootq = rootq;
+    h.wideq_stack = (uint32_t)std::max(1, needq);
+    h.wideq_width = (uint32_t)qwidth;
   }
   return true;
 }
