@@ -21,6 +21,9 @@ namespace rtd {
 #ifndef RT_WIDE_SPEC  // wide BVH in HBM: speculative while-while traversal (trace_wide)
 #define RT_WIDE_SPEC 1
 #endif
+#ifndef RT_WIDE_PREFETCH  // a triangle's words loaded with the record's first word (C4 358.9 -> 357.2 ms)
+#define RT_WIDE_PREFETCH 1
+#endif
 
 // Math policy. fp64 (the parity path): libm where the reference calls it (log), and division,
 // reciprocal and square root refined from the hardware estimates to about an ulp (below).
@@ -956,6 +959,9 @@ __device__ __forceinline__ bool trace_wide(const DevScene<float>& sc, const unsi
       sc.wide_spill[(uint32_t)(sp - (int)kWideLdsStack) * sc.spill_lanes + lane] = v;
     sp++;
   };
+  // (Round 3 measured three rewrites of push / pop / child below that the compiler's branchy code
+  // beat on C4 / C3: a branch-free push writing the entry either way, 358.9 -> 365.9 / 60.76 -> 61.84
+  // ms; the child code chosen by masks instead of ?:, 388.5 ms; a clamped LDS pop, neutral.)
   auto pop = [&]() -> uint32_t {
     --sp;
     if (LDSN || sp < (int)kWideLdsStack) return stk[sp * BLOCK];
@@ -975,20 +981,28 @@ __device__ __forceinline__ bool trace_wide(const DevScene<float>& sc, const unsi
   auto test_prims = [&](uint32_t w, uint32_t count) {
     for (uint32_t n = count; n > 0; n--) {
       const float4 h = prims[w];
+      // a kernel with triangles loads a record's next two words with its first (the word stream is
+      // padded, rt_scene.h), so a triangle costs one memory latency, not two: its kind is in word 0
+      [[maybe_unused]] float4 a1{}, a2{};
+      constexpr bool PF = TRI && RT_WIDE_PREFETCH;
+      if constexpr (PF) {
+        a1 = prims[w + 1];
+        a2 = prims[w + 2];
+      }
       const uint32_t e = __float_as_uint(h.w);
       const uint32_t ty = etype(e);
       float th;
       bool hit = false;
       if (SPH && (!(TRI || QUAD) || ty == E_SPHERE)) {
-        const float4 b = prims[w + 1];
+        const float4 b = PF ? a1 : prims[w + 1];
         w += 2;
         hit = sphere_test(mkv(h.x, h.y, h.z), mkv(b.x, b.y, b.z), b.w, MOV, o, d, time, tmin, tmax, e == excl_e, th);
       } else if (TRI && (!QUAD || ty == E_TRI)) {
-        const float4 a = prims[w + 1], b = prims[w + 2];
+        const float4 a = PF ? a1 : prims[w + 1], b = PF ? a2 : prims[w + 2];
         w += 3;
         hit = e != excl_e && tri_test(mkv(h.x, h.y, h.z), mkv(a.x, a.y, a.z), mkv(b.x, b.y, b.z), o, d, tmin, tmax, th);
       } else if (QUAD) {
-        const float4 nD = prims[w + 1], qa = prims[w + 2], qb = prims[w + 3];
+        const float4 nD = PF ? a1 : prims[w + 1], qa = PF ? a2 : prims[w + 2], qb = prims[w + 3];
         w += 4;
         hit = e != excl_e && quad_test(mkv(nD.x, nD.y, nD.z), nD.w, mkv(h.x, h.y, h.z), mkv(qa.x, qa.y, qa.z),
                                        mkv(qb.x, qb.y, qb.z), o, d, tmin, tmax, th);
@@ -1530,6 +1544,23 @@ __device__ __forceinline__ Onb<R> make_onb(V<R> n) {
   } else {
     V<R> a = (fabs(b.y.x) > R(0.9)) ? mkv(R(0), R(0), R(1)) : mkv(R(1), R(0), R(0));
     b.z = unit(cross(b.y, a));
+  }
+  b.x = cross(b.y, b.z);
+  return b;
+}
+// The onb of an axis-aligned normal n = +-e_A (every hit of the flat program): unit(n) = n and the
+// cross product before the second normalisation has length exactly 1, so this is make_onb without
+// its two normalisations -- bit-identical (the refined rsqrt of 1 is 1, and v * 1 = v), cheaper.
+template <class R>
+__device__ __forceinline__ Onb<R> make_onb_axis(V<R> n) {
+  Onb<R> b;
+  b.y = n;
+  if constexpr (sizeof(R) == 4) {
+    const bool ez = fabsf(b.y.x) > 0.9f;
+    b.z = mkv(ez ? b.y.y : 0.f, ez ? -b.y.x : b.y.z, ez ? 0.f : -b.y.y);
+  } else {
+    const V<R> a = (fabs(b.y.x) > R(0.9)) ? mkv(R(0), R(0), R(1)) : mkv(R(1), R(0), R(0));
+    b.z = cross(b.y, a);
   }
   b.x = cross(b.y, b.z);
   return b;

@@ -658,7 +658,7 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
         // gloss, specular branch (material.h:158-167): kDetermined, attenuation 1,
         // direction unit(lerp(smoothness, cosine-hemisphere sample about n, reflect(d_in, n)))
         js++;
-        const Onb<R> b = make_onb(n);
+        const Onb<R> b = FLAT ? make_onb_axis(n) : make_onb(n);
         const R r1 = U();
         const R r2 = U();
         const V<R> diffuse = onb_transform(b, cosine_dir(r1, r2));
@@ -669,7 +669,7 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
         const bool iso = m.kind == M_ISOTROPIC;
         const R iso_pdf = R(1) / (R(4) * Num<R>::pi());
         Onb<R> b;
-        if (!iso) b = make_onb(n);
+        if (!iso) b = FLAT ? make_onb_axis(n) : make_onb(n);
         const Light<R>* Lt = sc.light;  // read at the point of use (light_pdf, light_random)
         R pv;
         V<R> dir;
@@ -819,6 +819,9 @@ struct StackTrav {
 #ifndef RT_WIDE_WAVES_GLOBAL  // tree in HBM, 32-bit stack in LDS (C4 stand-in: 4 waves 519 ms, 5: 462; with the
 // speculative traversal 5: 424, 6: 412.5 -- 7 blocks of 24 KB stacks do not fit the 160 KB LDS)
 #define RT_WIDE_WAVES_GLOBAL 6
+#endif
+#ifndef RT_WIDE_TRIQUAD  // a kernel for triangle + quad scenes (else the all-kinds kernel): C4 358.9 -> 353.8 ms
+#define RT_WIDE_TRIQUAD 1
 #endif
 #ifndef RT_PARAM_RELOAD  // flat / linear / binary-BVH loops: parameters reloaded per segment
 #define RT_PARAM_RELOAD 1
@@ -1466,13 +1469,16 @@ void launch_wide_k(const Params<float>& p, uint32_t grid, hipStream_t st) {
                p.sc.wide_spill ? std::min<uint32_t>(grid, p.sc.spill_lanes / kBlock) : grid, st,
                wide_lds_bytes(p.sc, false));
 }
-// Kernel for the primitive kinds of the scene: spheres only (RTOW), triangles only (meshes), or all.
+// Kernel for the primitive kinds of the scene: spheres only (RTOW), triangles only or triangles and
+// quads (meshes, the C4 stand-in with its light), or all.
 inline void launch_wide(const Params<float>& p, uint32_t grid, hipStream_t st) {
   const uint32_t k = p.sc.wide_kinds;
   if (k == WK_SPHERE)
     launch_wide_k<true, false, false, false>(p, grid, st);
   else if (k == WK_TRI)
     launch_wide_k<false, true, false, false>(p, grid, st);
+  else if (RT_WIDE_TRIQUAD && k == (WK_TRI | WK_QUAD))  // a mesh under a quad light (the C4 stand-in)
+    launch_wide_k<false, true, true, false>(p, grid, st);
   else
     launch_wide_k<true, true, true, true>(p, grid, st);
 }

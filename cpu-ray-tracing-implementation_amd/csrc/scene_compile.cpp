@@ -1330,7 +1330,12 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
   // (r03j, ms/frame: float 4-wide 362.7, quantised 4-wide 386.5, 8-wide 506.0): the kernel there is
   // bound by VALU issue in traversal, and dequantising the planes (and for 8-wide, a 19-comparator
   // sort per visit) costs more than the smaller nodes and the halved fetch depth save.
-  const bool okq = (qwidth == 4 || qwidth == 8) && emitq(0, rootq, needq) && needq <= kWideStackMax;  SceneHeader& h = out->hdr;
+  const bool okq = (qwidth == 4 || qwidth == 8) && emitq(0, rootq, needq) && needq <= kWideStackMax;
+  // two zero words past the last record: kernels with triangles read a record's next two words with
+  // its first (trace_wide test_prims), past the end for a trailing sphere
+  words.push_back({0.f, 0.f, 0.f, 0.f});
+  words.push_back({0.f, 0.f, 0.f, 0.f});
+  SceneHeader& h = out->hdr;
   h.off_wnodes = append(out->blob32, wn);
   h.off_wprims = append(out->blob32, words);
   out->blob32.resize((out->blob32.size() + 255) & ~size_t(255));

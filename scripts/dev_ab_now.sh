@@ -1,0 +1,12 @@
+# Development: frame times of the current build on C2 (fp64, fp32), C3 and C4 (fp32).
+set -e
+mkdir -p gpurun_out/now
+run() {  # name, env, args
+  local v=$1 e=$2; shift 2
+  env $e timeout -k 10 300 python3 bench.py --no-cpu-baseline --alt-steps 0 "$@" > gpurun_out/now/$v.json 2>gpurun_out/now/$v.err
+  python3 -c "import json;d=json.load(open('gpurun_out/now/$v.json'));print('$v',d['ms_per_step'], d['value'], d['config'].get('grid_lanes'), d['config']['segments_per_sample'])"
+}
+run c2_f64 "" --config c2 --precision f64 --steps 10
+run c2_f32 "" --config c2 --precision f32 --steps 20
+run c3_f32 "" --config c3 --precision f32 --steps 5
+run c4_f32 "" --config c4 --precision f32 --steps 3
