@@ -568,13 +568,8 @@ __device__ __forceinline__ bool aquad_t(const R* f, V<R> o, V<R> d, V<R> inv, R 
   R pu = (comp<U>(o) + th * comp<U>(d)) - f[1];
   R pv = (comp<W>(o) + th * comp<W>(d)) - f[2];
   R a, b;
-  if constexpr (sizeof(R) == 8) {
-    a = fdiv(pu, f[5]);
-    b = fdiv(pv, f[6]);
-  } else {
-    a = pu * f[3];
-    b = pv * f[4];
-  }
+  a = pu * f[3];  // the stored reciprocals 1/u_U, 1/v_V (fp64: within an ulp of pu / u_U)
+  b = pv * f[4];
   if (!(R(0) <= a && a <= R(1) && R(0) <= b && b <= R(1))) return false;
   t = th;
   return true;
@@ -1620,7 +1615,7 @@ __device__ __forceinline__ R light_pdf(const Light<R>* Lp, V<R> o, V<R> dir, boo
     if (sizeof(R) == 4 && sampled) {
       t = R(1);
       hit = true;
-    } else if (sizeof(R) == 4 && aligned) {  // uniform branch
+    } else if (aligned) {  // uniform branch
       const LightAF<R> af = ld_here(reinterpret_cast<const LightAF<R>*>(Lp->af));
       const V<R> inv = rcp3(dir);
       switch (aligned) {
