@@ -67,6 +67,12 @@ constexpr int kBlock = 256;
 #ifndef RT_STACK_WAVES  // 4: the LDS limit of the LDS-node BVH kernel (32.8 KB per block); C3 151 -> 129 ms vs 3
 #define RT_STACK_WAVES 4
 #endif
+#ifndef RT_LINEAR_WAVES_F64  // fp64 linear programs: waves per SIMD the register budget is cut for (C5 fp64:
+#define RT_LINEAR_WAVES_F64 3   // none (2 waves) 3,605 ms/frame, 3: 2,865, 4: 3,885)
+#endif
+#ifndef RT_STACK_WAVES_F64  // fp64 binary BVH with its nodes in HBM (C4 fp64: none (2 waves) 2,019 ms/frame, 3: 1,964,
+#define RT_STACK_WAVES_F64 4  // 4: 1,704); with the nodes in LDS (C3 fp64) none: 260 ms, 3: 295, 4: 276
+#endif
 #ifndef RT_LINEAR_VOL_WAVES  // fp32 quad + volume linear program (C5), with slab-tested box() volumes: 1 (4 waves at
                              // 128 VGPRs) 1661 ms/frame, 5: 1567, 6: 2594 (spills)
 #define RT_LINEAR_VOL_WAVES 5
@@ -750,7 +756,7 @@ struct LinearTrav {
   static constexpr int kStack = 0;
   // waves per SIMD the register budget is cut for (occupancy hides the shading loads); the
   // lean quad-only program fits 96 VGPRs with a small spill, the others would spill heavily
-  static constexpr int kWaves = sizeof(R) != 4 ? 1
+  static constexpr int kWaves = sizeof(R) != 4 ? RT_LINEAR_WAVES_F64
                                  : (!SPH && !TRI && !VOL) ? RT_LINEAR_WAVES
                                  : (!SPH && !TRI && VOL)  ? RT_LINEAR_VOL_WAVES
                                                           : 1;
@@ -797,7 +803,7 @@ template <class R, int STACK, bool LDSN = false>
 struct StackTrav {
   static constexpr int kStack = STACK;
   static constexpr int kLdsNodes = LDSN ? (int)kLdsNodeMax : 0;
-  static constexpr int kWaves = sizeof(R) == 4 ? RT_STACK_WAVES : 1;  // fp32: occupancy over a small spill
+  static constexpr int kWaves = sizeof(R) == 4 ? RT_STACK_WAVES : (LDSN ? 1 : RT_STACK_WAVES_F64);  // occupancy over a small spill
   static constexpr bool kFlat = false;
   static constexpr bool kWide = false;
   static constexpr bool kColdLds = false;  // its LDS holds the traversal stacks

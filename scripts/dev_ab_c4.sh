@@ -1,6 +1,4 @@
-# Development A/B of trace_wide code shapes on C4 / C3 fp32 (v0: all round-3 switches off; v1: child by
-# masks; v2: clamped pop; v3: branch-free push; v4: triangle words prefetched; v5: triangle+quad kernel).
-#   bash scripts/dev_ab_c4.sh v0 v1 ...
+# Development A/B on C4 fp32: pause thresholds 40 / 56 (default 48) and 22 LDS stack entries at 7 waves.
 set -e
 mkdir -p gpurun_out/abc4
 B=cpu-ray-tracing-implementation_amd/build
@@ -9,7 +7,6 @@ run() {  # name, env, args
   env $e timeout -k 10 300 python3 bench.py --no-cpu-baseline --alt-steps 0 "$@" > gpurun_out/abc4/$v.json 2>gpurun_out/abc4/$v.err
   python3 -c "import json;d=json.load(open('gpurun_out/abc4/$v.json'));print('$v',d['ms_per_step'], d['value'], d['config'].get('grid_lanes'), d['config']['segments_per_sample'])"
 }
-for v in "$@"; do
-  run c4_$v "RT_HIP_LIB=$B/librt_hip_$v.so" --config c4 --precision f32 --steps 3
-  run c3_$v "RT_HIP_LIB=$B/librt_hip_$v.so" --config c3 --precision f32 --steps 5
-done
+run c4_base "" --config c4 --precision f32 --steps 3
+for v in p40 p56 s22; do run c4_$v "RT_HIP_LIB=$B/librt_hip_$v.so" --config c4 --precision f32 --steps 3; done
+run c5_f64 "" --config c5 --precision f64 --steps 2
