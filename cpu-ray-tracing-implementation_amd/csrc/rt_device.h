@@ -261,6 +261,25 @@ struct Keys {
 };
 
 // ------------------------------------------------------------------ scene view
+// A word of the wide BVH's primitive stream (rt_scene.h WNode): 16 bytes of floats in the fp32
+// blob, 32 bytes of doubles in the fp64 one (same word indices, so the leaf codes are shared); the
+// primitive's entry is in the bits of w (the low 32 bits of the double).
+template <class R>
+struct WWord;
+template <>
+struct WWord<float> {
+  using T = float4;
+};
+struct alignas(32) double4w {
+  double x, y, z, w;
+};
+template <>
+struct WWord<double> {
+  using T = double4w;
+};
+__device__ __forceinline__ uint32_t wentry(const float4& h) { return __float_as_uint(h.w); }
+__device__ __forceinline__ uint32_t wentry(const double4w& h) { return (uint32_t)__double_as_longlong(h.w); }
+
 template <class R>
 struct DevScene {
   const Quad<R>* quads;
@@ -286,9 +305,10 @@ struct DevScene {
   const double* texdata;  // procedural-texture tables (Texture::data)
   const uint8_t* images;  // picture-texture pixels (Texture::data)
   int32_t has_procedural; // any perlin / value / worley / voronoi texture: the EXT kernels
-  // wide BVH (fp32; rt_scene.h WNode): nodes, primitive words, root code, stack need, WK_* kinds
+  // wide BVH (rt_scene.h WNode; float boxes in both blobs): nodes, primitive words, root code,
+  // stack need, WK_* kinds
   const WNode* wnodes;
-  const float4* wprims;
+  const typename WWord<R>::T* wprims;
   uint32_t n_wnodes, n_wprim_words, wroot, wide_stack, wide_kinds;
   int32_t has_wide;
   uint32_t wide_big;  // primitives at the head of the word stream, tested before the tree
@@ -845,10 +865,11 @@ constexpr uint32_t kWNodeLdsStride = 144;
 // the wave's lanes that entered are finished and waiting: the persistent kernel then shades those
 // together and the paused lanes carry on beside the new rays (trace_wide callers in rt_kernels.hip).
 // Without the pause a wave would traverse until its slowest ray is done, its finished lanes idle.
-struct WideRay {
+template <class R>
+struct WideRayT {
   uint32_t cur;   // node index or leaf code to visit next
   int32_t sp;     // entries on the LDS stack
-  float tmax;     // closest hit so far
+  R tmax;         // closest hit so far
   uint32_t e;     // its entry (kNoHit: none)
   uint32_t fresh; // 1: the head primitives (DevScene::wide_big) are still to be tested
 };
@@ -938,15 +959,34 @@ __device__ __forceinline__ uint32_t wide8_child(uint32_t key, const uint4& c0, c
   const uint32_t lo = (key & 1u) ? c.y : c.x, hi = (key & 1u) ? c.w : c.z;
   return (key & 2u) ? hi : lo;
 }
-template <bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN, int BLOCK, int PAUSE, int QN = 0>
-__device__ __forceinline__ bool trace_wide(const DevScene<float>& sc, const unsigned char* lds_nodes,
-                                           const float4* lds_prims, V<float> o, V<float> d, float time,
-                                           uint32_t excl_e, WStackT<LDSN>* stk, WideRay& ry) {
-  static_assert(QN == 0 || (!LDSN && RT_WIDE_SPEC), "quantised nodes are traversed speculatively, from HBM");
+// fp64 rays (round 3) traverse the same float boxes: the ray is rounded to float for the slab tests
+// and every slab is widened by the distance the rounding moved the origin along that axis, |delta_a|
+// / |d_a| (delta = o - float(o), exact in double, scaled by 1 + 2^-20), the direction's rounding
+// being covered, like the fp32 path's own, by the relative box_slack of the exit distance; the
+// lower bound is 0.00099 instead of 0.001. The boxes only cull: the primitive tests are the fp64
+// ones of the other fp64 traversals, so the closest hit is theirs (exact-t ties aside).
+template <class R, bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN, int BLOCK, int PAUSE, int QN = 0>
+__device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned char* lds_nodes,
+                                           const typename WWord<R>::T* lds_prims, V<R> ro, V<R> rd, R time,
+                                           uint32_t excl_e, WStackT<LDSN>* stk, WideRayT<R>& ry) {
+  using WW = typename WWord<R>::T;
+  constexpr bool F64 = sizeof(R) == 8;
+  static_assert(QN == 0 || (!LDSN && RT_WIDE_SPEC && !F64), "quantised nodes: fp32, traversed speculatively, from HBM");
   constexpr uint32_t kLeafBit = LDSN ? kWLeaf16 : kWLeaf;
-  const float tmin = 0.001f;
-  const V<float> inv = box_inv(d);
-  const float4* prims = LDSN ? lds_prims : sc.wprims;
+  const R tmin = R(0.001);
+  const float tmin_box = F64 ? 0.00099f : 0.001f;
+  const V<float> o = mkv((float)ro.x, (float)ro.y, (float)ro.z);
+  const V<float> inv = box_inv(mkv((float)rd.x, (float)rd.y, (float)rd.z));
+  [[maybe_unused]] float wx = 0.f, wy = 0.f, wz = 0.f;  // fp64: the slab widening per axis
+  if constexpr (F64) {
+    auto widen = [](double dlt, float iv) {
+      return dlt == 0.0 ? 0.f : fabsf((float)dlt * iv) * (1.0f + 9.5367431640625e-07f);
+    };
+    wx = widen(ro.x - (double)o.x, inv.x);
+    wy = widen(ro.y - (double)o.y, inv.y);
+    wz = widen(ro.z - (double)o.z, inv.z);
+  }
+  const WW* prims = LDSN ? lds_prims : sc.wprims;
   uint32_t keep_going = 0;  // pause at or below this many traversing lanes
   if constexpr (PAUSE < 64) {
     const uint32_t entered = (uint32_t)__popcll(__ballot(1));
@@ -954,7 +994,7 @@ __device__ __forceinline__ bool trace_wide(const DevScene<float>& sc, const unsi
   }
   uint32_t cur = ry.cur;
   int sp = ry.sp;
-  float tmax = ry.tmax;
+  R tmax = ry.tmax;
   uint32_t e_best = ry.e;
   // the lane's stack: LDS, and for a tree in HBM its spill area past kWideLdsStack entries
   [[maybe_unused]] const uint32_t lane = blockIdx.x * BLOCK + threadIdx.x;
@@ -977,41 +1017,48 @@ __device__ __forceinline__ bool trace_wide(const DevScene<float>& sc, const unsi
     const float tx0 = (lx - o.x) * inv.x, tx1 = (hx - o.x) * inv.x;
     const float ty0 = (ly - o.y) * inv.y, ty1 = (hy - o.y) * inv.y;
     const float tz0 = (lz - o.z) * inv.z, tz1 = (hz - o.z) * inv.z;
-    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
-    const float tf =
-        fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax)) * Num<float>::box_slack();
+    float tn, tf;
+    if constexpr (F64) {
+      tn = fmaxf(fmaxf(fminf(tx0, tx1) - wx, fminf(ty0, ty1) - wy), fmaxf(fminf(tz0, tz1) - wz, tmin_box));
+      tf = fminf(fminf(fmaxf(tx0, tx1) + wx, fmaxf(ty0, ty1) + wy), fminf(fmaxf(tz0, tz1) + wz, (float)tmax)) *
+           Num<float>::box_slack();
+    } else {
+      tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin_box));
+      tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), (float)tmax)) *
+           Num<float>::box_slack();
+    }
     // tn >= tmin > 0: the bit pattern orders like the value; the low 2 bits carry the slot
     return tn <= tf ? ((__float_as_uint(tn) & ~3u) | c) : 0xFFFFFFFFu;
   };
   // the primitives of a leaf (or of the head list), their records from word w on
   auto test_prims = [&](uint32_t w, uint32_t count) {
     for (uint32_t n = count; n > 0; n--) {
-      const float4 h = prims[w];
+      const WW h = prims[w];
       // a kernel with triangles loads a record's next two words with its first (the word stream is
       // padded, rt_scene.h), so a triangle costs one memory latency, not two: its kind is in word 0
-      [[maybe_unused]] float4 a1{}, a2{};
+      [[maybe_unused]] WW a1{}, a2{};
       constexpr bool PF = TRI && RT_WIDE_PREFETCH;
       if constexpr (PF) {
         a1 = prims[w + 1];
         a2 = prims[w + 2];
       }
-      const uint32_t e = __float_as_uint(h.w);
+      const uint32_t e = wentry(h);
       const uint32_t ty = etype(e);
-      float th;
+      R th;
       bool hit = false;
       if (SPH && (!(TRI || QUAD) || ty == E_SPHERE)) {
-        const float4 b = PF ? a1 : prims[w + 1];
+        const WW b = PF ? a1 : prims[w + 1];
         w += 2;
-        hit = sphere_test(mkv(h.x, h.y, h.z), mkv(b.x, b.y, b.z), b.w, MOV, o, d, time, tmin, tmax, e == excl_e, th);
+        hit = sphere_test(mkv(h.x, h.y, h.z), mkv(b.x, b.y, b.z), b.w, MOV, ro, rd, time, tmin, tmax, e == excl_e, th);
       } else if (TRI && (!QUAD || ty == E_TRI)) {
-        const float4 a = PF ? a1 : prims[w + 1], b = PF ? a2 : prims[w + 2];
+        const WW a = PF ? a1 : prims[w + 1], b = PF ? a2 : prims[w + 2];
         w += 3;
-        hit = e != excl_e && tri_test(mkv(h.x, h.y, h.z), mkv(a.x, a.y, a.z), mkv(b.x, b.y, b.z), o, d, tmin, tmax, th);
+        hit = e != excl_e && tri_test(mkv(h.x, h.y, h.z), mkv(a.x, a.y, a.z), mkv(b.x, b.y, b.z), ro, rd, tmin, tmax, th);
       } else if (QUAD) {
-        const float4 nD = PF ? a1 : prims[w + 1], qa = PF ? a2 : prims[w + 2], qb = prims[w + 3];
+        const WW nD = PF ? a1 : prims[w + 1], qa = PF ? a2 : prims[w + 2], qb = prims[w + 3];
         w += 4;
         hit = e != excl_e && quad_test(mkv(nD.x, nD.y, nD.z), nD.w, mkv(h.x, h.y, h.z), mkv(qa.x, qa.y, qa.z),
-                                       mkv(qb.x, qb.y, qb.z), o, d, tmin, tmax, th);
+                                       mkv(qb.x, qb.y, qb.z), ro, rd, tmin, tmax, th);
       }
       if (hit) {
         tmax = th;

@@ -841,23 +841,31 @@ struct StackTrav {
 #ifndef RT_SHADE_BATCH_GLOBAL  // the same for trees in HBM (speculative traversal): C4 stand-in 413.6 ms/frame
 #define RT_SHADE_BATCH_GLOBAL 48  // never pausing, 415.2 / 370.8 / 363.8 / 362.5 / 368.4 / 379.6 at 16/32/40/48/56/60
 #endif
-template <bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN, int QN = 0>
+#ifndef RT_WIDE_WAVES_F64  // fp64 rays over the wide tree (round 3): tree in LDS / in HBM
+#define RT_WIDE_WAVES_F64 1
+#endif
+#ifndef RT_WIDE_WAVES_GLOBAL_F64
+#define RT_WIDE_WAVES_GLOBAL_F64 4
+#endif
+template <class R, bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN, int QN = 0>
 struct WideTrav {
   static constexpr int kStack = 0;
   static constexpr int kLdsNodes = 0;
-  static constexpr int kWaves = LDSN ? RT_WIDE_WAVES : RT_WIDE_WAVES_GLOBAL;
+  static constexpr int kWaves = sizeof(R) == 4 ? (LDSN ? RT_WIDE_WAVES : RT_WIDE_WAVES_GLOBAL)
+                                               : (LDSN ? RT_WIDE_WAVES_F64 : RT_WIDE_WAVES_GLOBAL_F64);
   static constexpr bool kFlat = false;
   static constexpr bool kWide = true;
   static constexpr bool kColdLds = false;  // its LDS holds the tree and the stacks
   using StackT = WStackT<LDSN>;
+  using WW = typename WWord<R>::T;
   // LDS layout: [nodes, kWNodeLdsStride each][primitive words][stack: entries x kBlock of StackT]
   __host__ __device__ static uint32_t stack_offset(uint32_t n_wnodes, uint32_t n_words) {
-    return LDSN ? n_wnodes * kWNodeLdsStride + n_words * 16u : 0u;
+    return LDSN ? n_wnodes * kWNodeLdsStride + n_words * (uint32_t)sizeof(WW) : 0u;
   }
-  __host__ __device__ static uint32_t root(const DevScene<float>& sc) {
+  __host__ __device__ static uint32_t root(const DevScene<R>& sc) {
     return QN ? sc.wrootq : (LDSN ? wide_code16(sc.wroot) : sc.wroot);
   }
-  __device__ __forceinline__ static StackT* fill(const DevScene<float>& sc, uint4* lds) {
+  __device__ __forceinline__ static StackT* fill(const DevScene<R>& sc, uint4* lds) {
     unsigned char* base = (unsigned char*)lds;
     if constexpr (LDSN) {
       const uint4* gn = (const uint4*)sc.wnodes;  // 8 words of 16 B per node, the last one padding
@@ -870,18 +878,19 @@ struct WideTrav {
       }
       uint4* pw = (uint4*)(base + sc.n_wnodes * kWNodeLdsStride);
       const uint4* gp = (const uint4*)sc.wprims;
-      for (uint32_t j = threadIdx.x; j < sc.n_wprim_words; j += kBlock) pw[j] = gp[j];
+      const uint32_t n16 = sc.n_wprim_words * (uint32_t)(sizeof(WW) / 16);
+      for (uint32_t j = threadIdx.x; j < n16; j += kBlock) pw[j] = gp[j];
       __syncthreads();
     }
     return (StackT*)(base + stack_offset(sc.n_wnodes, sc.n_wprim_words));
   }
   // Advance the ray of s (false: paused, see trace_wide)
   template <class PS>
-  __device__ __forceinline__ static bool steps(const DevScene<float>& sc, const Node<float>* lds, const PS& s,
-                                               StackT* stk, WideRay& ry) {
+  __device__ __forceinline__ static bool steps(const DevScene<R>& sc, const Node<R>* lds, const PS& s, StackT* stk,
+                                               WideRayT<R>& ry) {
     const unsigned char* base = (const unsigned char*)lds;
-    return trace_wide<SPH, TRI, QUAD, MOV, LDSN, kBlock, LDSN ? RT_SHADE_BATCH : RT_SHADE_BATCH_GLOBAL, QN>(
-        sc, base, (const float4*)(base + sc.n_wnodes * kWNodeLdsStride), s.o, s.d, s.tm, s.xe, stk, ry);
+    return trace_wide<R, SPH, TRI, QUAD, MOV, LDSN, kBlock, LDSN ? RT_SHADE_BATCH : RT_SHADE_BATCH_GLOBAL, QN>(
+        sc, base, (const WW*)(base + sc.n_wnodes * kWNodeLdsStride), s.o, s.d, s.tm, s.xe, stk, ry);
   }
 };
 
@@ -1007,7 +1016,7 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
       // resumable traversal: a ray paused with the wave's laggards carries on after the others shade
       using StackT = typename Trav::StackT;
       const uint32_t root = Trav::root(p.sc);
-      WideRay ry{root, 0, Num<float>::inf(), kNoHit, 1u};
+      WideRayT<R> ry{root, 0, Num<R>::inf(), kNoHit, 1u};
 #if RT_WIDE_RELOAD
       using KP = const __attribute__((address_space(4))) Params<R>*;
       const KP kp0 = (KP)__builtin_amdgcn_kernarg_segment_ptr();
@@ -1026,9 +1035,9 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
           atomicOr(q.fault, 1u);
           break;
         }
-        const float t = ry.tmax;
+        const R t = ry.tmax;
         const uint32_t e = ry.e;
-        ry = WideRay{root, 0, Num<float>::inf(), kNoHit, 1u};
+        ry = WideRayT<R>{root, 0, Num<R>::inf(), kNoHit, 1u};
         if (!shade<R, CAMX, false>(q, s, t, e, -1, 0)) break;
       }
     } else {
@@ -1396,7 +1405,7 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
   s.has_procedural = h.n_texdata > 0 || h.has_cell_noise;
   s.has_wide = (int32_t)h.has_wide;
   s.wnodes = (const WNode*)at(h.off_wnodes);
-  s.wprims = (const float4*)at(h.off_wprims);
+  s.wprims = (const typename WWord<R>::T*)at(h.off_wprims);
   s.n_wnodes = h.n_wnodes;
   s.n_wprim_words = h.n_wprim_words;
   s.wroot = h.wroot;
@@ -1450,43 +1459,52 @@ void launch_one(KernelT kern, Params<R> p, uint32_t grid, hipStream_t st, size_t
 
 // Dynamic LDS of a wide-BVH launch: the whole tree when it fits the budget (LDSN), else the stack only.
 constexpr size_t kWideLdsBudget = 40u << 10;  // bytes per 256-lane block: 4 blocks per CU of 160 KiB
-inline size_t wide_lds_bytes(const DevScene<float>& sc, bool ldsn, bool w8 = false) {
+template <class R>
+inline size_t wide_lds_bytes(const DevScene<R>& sc, bool ldsn, bool w8 = false) {
   // an LDS tree: every entry in LDS, uint16; a tree in HBM: up to kWideLdsStack uint32 entries (the rest spill)
   const size_t stack = ldsn ? (size_t)sc.wide_stack * kBlock * 2u
                             : (size_t)std::min<uint32_t>(w8 ? sc.wideq_stack : sc.wide_stack, kWideLdsStack) * kBlock * 4u;
-  return (ldsn ? (size_t)sc.n_wnodes * kWNodeLdsStride + (size_t)sc.n_wprim_words * 16u : 0u) + stack;
+  return (ldsn ? (size_t)sc.n_wnodes * kWNodeLdsStride + (size_t)sc.n_wprim_words * sizeof(typename WWord<R>::T) : 0u) +
+         stack;
 }
-template <bool SPH, bool TRI, bool QUAD, bool MOV>
-void launch_wide_k(const Params<float>& p, uint32_t grid, hipStream_t st) {
+template <class R, bool SPH, bool TRI, bool QUAD, bool MOV>
+void launch_wide_k(const Params<R>& p, uint32_t grid, hipStream_t st) {
   const size_t full = wide_lds_bytes(p.sc, true);
+  const uint32_t spill_grid = p.sc.wide_spill ? std::min<uint32_t>(grid, p.sc.spill_lanes / kBlock) : grid;
   // LDS-resident trees use 16-bit child codes (wide_code16): node offset (index x 9) < 2^15, first word < 2^12
-  if (full <= kWideLdsBudget && p.sc.n_wnodes * kWNodeLdsUnits < 0x8000u && p.sc.n_wprim_words <= 0x1000u)
-    launch_one(k_persist_occ<float, WideTrav<SPH, TRI, QUAD, MOV, true>, false>, p, grid, st, full);
-  else if (p.sc.wideq_width == 4)  // the quantised tree (the spill area holds spill_lanes lanes: never launch more)
-    launch_one(k_persist_occ<float, WideTrav<SPH, TRI, QUAD, MOV, false, 4>, false>, p,
-               p.sc.wide_spill ? std::min<uint32_t>(grid, p.sc.spill_lanes / kBlock) : grid, st,
-               wide_lds_bytes(p.sc, false, true));
-  else if (p.sc.wideq_width == 8)
-    launch_one(k_persist_occ<float, WideTrav<SPH, TRI, QUAD, MOV, false, 8>, false>, p,
-               p.sc.wide_spill ? std::min<uint32_t>(grid, p.sc.spill_lanes / kBlock) : grid, st,
-               wide_lds_bytes(p.sc, false, true));
-  else
-    launch_one(k_persist_occ<float, WideTrav<SPH, TRI, QUAD, MOV, false>, false>, p,
-               p.sc.wide_spill ? std::min<uint32_t>(grid, p.sc.spill_lanes / kBlock) : grid, st,
-               wide_lds_bytes(p.sc, false));
+  if (full <= kWideLdsBudget && p.sc.n_wnodes * kWNodeLdsUnits < 0x8000u && p.sc.n_wprim_words <= 0x1000u) {
+    launch_one(k_persist_occ<R, WideTrav<R, SPH, TRI, QUAD, MOV, true>, false>, p, grid, st, full);
+    return;
+  }
+  if constexpr (sizeof(R) == 4) {  // the quantised trees (fp32; opt-in, RT_DEV_WIDEQ)
+    if (p.sc.wideq_width == 4) {
+      launch_one(k_persist_occ<R, WideTrav<R, SPH, TRI, QUAD, MOV, false, 4>, false>, p, spill_grid, st,
+                 wide_lds_bytes(p.sc, false, true));
+      return;
+    }
+    if (p.sc.wideq_width == 8) {
+      launch_one(k_persist_occ<R, WideTrav<R, SPH, TRI, QUAD, MOV, false, 8>, false>, p, spill_grid, st,
+                 wide_lds_bytes(p.sc, false, true));
+      return;
+    }
+  }
+  // the spill area holds spill_lanes lanes: never launch more (the resident grid is below it)
+  launch_one(k_persist_occ<R, WideTrav<R, SPH, TRI, QUAD, MOV, false>, false>, p, spill_grid, st,
+             wide_lds_bytes(p.sc, false));
 }
 // Kernel for the primitive kinds of the scene: spheres only (RTOW), triangles only or triangles and
 // quads (meshes, the C4 stand-in with its light), or all.
-inline void launch_wide(const Params<float>& p, uint32_t grid, hipStream_t st) {
+template <class R>
+inline void launch_wide(const Params<R>& p, uint32_t grid, hipStream_t st) {
   const uint32_t k = p.sc.wide_kinds;
   if (k == WK_SPHERE)
-    launch_wide_k<true, false, false, false>(p, grid, st);
+    launch_wide_k<R, true, false, false, false>(p, grid, st);
   else if (k == WK_TRI)
-    launch_wide_k<false, true, false, false>(p, grid, st);
+    launch_wide_k<R, false, true, false, false>(p, grid, st);
   else if (RT_WIDE_TRIQUAD && k == (WK_TRI | WK_QUAD))  // a mesh under a quad light (the C4 stand-in)
-    launch_wide_k<false, true, true, false>(p, grid, st);
+    launch_wide_k<R, false, true, true, false>(p, grid, st);
   else
-    launch_wide_k<true, true, true, true>(p, grid, st);
+    launch_wide_k<R, true, true, true, true>(p, grid, st);
 }
 template <class R, class Trav>
 void launch_k(const Params<R>& p, uint32_t grid, hipStream_t st) {
@@ -1526,10 +1544,10 @@ void launch_step(const Params<R>& p, int stack, bool sph, bool tri, uint32_t gri
       launch_k<R, LinearTrav<R, true, false, false>>(p, grid, st);
     else
       launch_k<R, LinearTrav<R, true, true, true>>(p, grid, st);
+  } else if (p.sc.has_wide && p.persist && p.cam_mode == RT_CAM_PERSPECTIVE && !p.sc.has_procedural) {
+    launch_wide(p, grid, st);  // the wide BVH (persistent schedule, base kernels; fp64 rays since round 3)
   } else if constexpr (sizeof(R) == 4) {
-    if (p.sc.has_wide && p.persist && p.cam_mode == RT_CAM_PERSPECTIVE && !p.sc.has_procedural) {
-      launch_wide(p, grid, st);  // the wide BVH (persistent schedule, base kernels)
-    } else if (p.sc.n_nodes <= kLdsNodeMax && stack <= 16) {
+    if (p.sc.n_nodes <= kLdsNodeMax && stack <= 16) {
       launch_k<R, StackTrav<R, 16, true>>(p, grid, st);
     } else if (stack <= 8) {
       launch_k<R, StackTrav<R, 8>>(p, grid, st);
@@ -1662,7 +1680,7 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     Params<R> p{};
     p.sc = dev_scene<R>(hdr, sbase);
     const uint32_t wide_need = std::max(hdr.wide_stack, hdr.wideq_width ? hdr.wideq_stack : 0u);
-    if (!f64 && hdr.has_wide && wide_need > kWideLdsStack) {
+    if (hdr.has_wide && wide_need > kWideLdsStack) {
       // a deep wide tree: a spill area of (need - kWideLdsStack) entries for every lane the chip can hold
       int ncu = 0;
       RT_HIP(c, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));

@@ -1138,32 +1138,48 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
     float x, y, z, w;
   };
   std::vector<W4> words;
+  // the same stream in double for the fp64 blob (fp64 rays over the same float boxes, rt_device.h
+  // trace_wide): word for word, so the leaf codes serve both; the entry in the low bits of w
+  struct W8 {
+    double x, y, z, w;
+  };
+  std::vector<W8> words64;
   uint32_t kinds = 0;
   auto bits = [](uint32_t u) {
     float f;
     std::memcpy(&f, &u, 4);
     return f;
   };
+  auto bits64 = [](uint32_t u) {
+    const uint64_t v = u;
+    double f;
+    std::memcpy(&f, &v, 8);
+    return f;
+  };
   auto put_prim = [&](uint32_t e) {  // the record of one primitive (rt_scene.h WNode)
     const uint32_t ix = epay(e);
+    auto put = [&](const double* v, double w, bool entry) {
+      words.push_back({(float)v[0], (float)v[1], (float)v[2], entry ? bits(e) : (float)w});
+      words64.push_back({v[0], v[1], v[2], entry ? bits64(e) : w});
+    };
     if (etype(e) == E_SPHERE) {
       const Sphere<double>& s = spheres_[ix];
       kinds |= WK_SPHERE | (s.moving ? WK_MOVING : 0u);
-      words.push_back({(float)s.c1[0], (float)s.c1[1], (float)s.c1[2], bits(e)});
-      words.push_back({(float)s.dc[0], (float)s.dc[1], (float)s.dc[2], (float)s.r});
+      put(s.c1, 0, true);
+      put(s.dc, s.r, false);
     } else if (etype(e) == E_TRI) {
       const Tri<double>& t = tris_[ix];
       kinds |= WK_TRI;
-      words.push_back({(float)t.p0[0], (float)t.p0[1], (float)t.p0[2], bits(e)});
-      words.push_back({(float)t.e1[0], (float)t.e1[1], (float)t.e1[2], 0.f});
-      words.push_back({(float)t.e2[0], (float)t.e2[1], (float)t.e2[2], 0.f});
+      put(t.p0, 0, true);
+      put(t.e1, 0, false);
+      put(t.e2, 0, false);
     } else if (etype(e) == E_QUAD) {
       const Quad<double>& q = quads_[ix];
       kinds |= WK_QUAD;
-      words.push_back({(float)q.q[0], (float)q.q[1], (float)q.q[2], bits(e)});
-      words.push_back({(float)q.n[0], (float)q.n[1], (float)q.n[2], (float)q.D});
-      words.push_back({(float)q.a[0], (float)q.a[1], (float)q.a[2], 0.f});
-      words.push_back({(float)q.b[0], (float)q.b[1], (float)q.b[2], 0.f});
+      put(q.q, 0, true);
+      put(q.n, q.D, false);
+      put(q.a, 0, false);
+      put(q.b, 0, false);
     } else {
       return false;
     }
@@ -1335,6 +1351,22 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
   // its first (trace_wide test_prims), past the end for a trailing sphere
   words.push_back({0.f, 0.f, 0.f, 0.f});
   words.push_back({0.f, 0.f, 0.f, 0.f});
+  words64.push_back({0, 0, 0, 0});
+  words64.push_back({0, 0, 0, 0});
+  {  // the fp64 blob: the same float nodes, the double words
+    SceneHeader& h = out->hdr64;
+    h.off_wnodes = append(out->blob64, wn);
+    h.off_wprims = append(out->blob64, words64);
+    out->blob64.resize((out->blob64.size() + 255) & ~size_t(255));
+    h.bytes = out->blob64.size();
+    h.n_wnodes = (uint32_t)wn.size();
+    h.n_wprim_words = (uint32_t)words64.size();
+    h.wroot = root;
+    h.wide_stack = (uint32_t)std::max(1, need);
+    h.wide_kinds = kinds;
+    h.wide_big = (uint32_t)big.size();
+    h.has_wide = 1;
+  }
   SceneHeader& h = out->hdr;
   h.off_wnodes = append(out->blob32, wn);
   h.off_wprims = append(out->blob32, words);
@@ -1573,7 +1605,7 @@ bool Compiler::run(CompiledScene* out, std::string* err) {
   // the wide BVH (fp32) when the world is a BVH over world-level primitives only
   bool prims_only = etype(root.entry) == E_NODE;
   for (const Item& it : top) prims_only = prims_only && etype(it.entry) <= E_TRI;
-  if (prims_only && !wide_bvh(top, out)) out->hdr.has_wide = 0;
+  if (prims_only && !wide_bvh(top, out)) out->hdr.has_wide = out->hdr64.has_wide = 0;
   for (SceneHeader* h : {&out->hdr, &out->hdr64}) {
     h->has_cell_noise = cell_noise_ ? 1 : 0;
     h->root = root.entry;

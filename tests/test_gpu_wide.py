@@ -152,3 +152,37 @@ def test_other_hbm_trees_match_binary(ctx, tmp_path, monkeypatch, wq):
     differ = np.abs(wide - binary).max(-1) > 0
     assert differ.mean() < 5e-3, int(differ.sum())
     assert (rmse(wide, binary) < 1e-4).all(), rmse(wide, binary)
+
+
+def both_traversals_f64(ctx, desc, cam, spp, depth, seed):
+    ctx.upload(desc)
+    wide = ctx.render(cam, spp, depth, seed=seed, precision=abi.RT_PREC_F64)
+    binary = ctx.render(cam, spp, depth, seed=seed, precision=abi.RT_PREC_F64, traversal=abi.RT_TRAV_ORDERED)
+    return wide, binary
+
+
+@pytest.mark.parametrize("which", ["rtow", "mixed", "sponza"])
+def test_wide_fp64_matches_binary_and_oracle(ctx, which, tmp_path, monkeypatch):
+    # fp64 rays over the float boxes (round 3): the slabs are widened for the rounding of the ray to float,
+    # so they only cull; the primitive tests are the fp64 ones, and the closest hits equal the fp64 binary
+    # BVH's (ties aside) -- the LDS-resident sphere tree (rtow), the all-kinds kernel (mixed) and the tree
+    # in HBM with its spill area (the Sponza stand-in)
+    if which == "rtow":
+        desc, cam, _, _ = scenes.rtow(width=64, aspect=1.5)
+        spp, depth, seed = 8, 50, 5
+    elif which == "mixed":
+        desc, cam = mixed_scene(3, False)
+        spp, depth, seed = 16, 10, 2
+    else:
+        from rt_amd import synth_gltf
+        monkeypatch.setenv("RT_SPONZA_GLTF", synth_gltf.write_sponza_standin(str(tmp_path)))
+        cs = plugin.ConfigScene("sponza", 64, 16.0 / 9.0)
+        desc, cam, spp, depth, seed = cs.desc, cs.cam, 4, 5, 3
+    wide, binary = both_traversals_f64(ctx, desc, cam, spp, depth, seed)
+    assert np.isfinite(wide).all()
+    differ = np.abs(wide - binary).max(-1) > 1e-9 * np.maximum(1.0, np.abs(binary).max(-1))
+    assert differ.mean() < 5e-3, int(differ.sum())
+    if which != "sponza":  # (the oracle's x-median tree over 262k triangles takes minutes)
+        ref, _ = oracle.render(oracle.from_desc(desc), cam, spp, depth, seed=seed, threads=8)
+        bad = (np.abs(wide - ref) > 1e-9 * np.maximum(1.0, np.abs(ref))).any(-1)
+        assert bad.mean() < 5e-3, (int(bad.sum()), float(np.abs(wide - ref).max()))
