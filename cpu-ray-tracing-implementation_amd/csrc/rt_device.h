@@ -1357,13 +1357,15 @@ __device__ __forceinline__ void flat_quad_test(const FlatQuadT<R>& r, int32_t id
 template <int A, class R>
 __device__ __forceinline__ void flat_quads(const FlatQuadT<R>* q, uint32_t n, int32_t base, V<R> o, V<R> d,
                                            V<R> inv, R tmin, R& tmax, int32_t& best, uint64_t xkey) {
-  const FlatQuad2<R>* q2 = reinterpret_cast<const FlatQuad2<R>*>(q);
+  // pairs of records in one scalar load each, then the odd one (round 3: groups are no longer padded
+  // to pairs with never-hit records -- Cornell's y and z groups had one each, 2 of 8 quad tests)
 #pragma unroll 1
-  for (uint32_t k = 0; k < n; k += 2) {
-    const FlatQuad2<R> r = ld_uniform(q2, k >> 1);
+  for (uint32_t k = 0; k + 1 < n; k += 2) {
+    const FlatQuad2<R> r = ld_uniform(reinterpret_cast<const FlatQuad2<R>*>(q + k), 0);
     flat_quad_test<A>(r.a, base + (int32_t)k, o, d, inv, tmin, tmax, best, xkey);
     flat_quad_test<A>(r.b, base + (int32_t)k + 1, o, d, inv, tmin, tmax, best, xkey);
   }
+  if (n & 1u) flat_quad_test<A>(ld_uniform(q, n - 1), base + (int32_t)(n - 1), o, d, inv, tmin, tmax, best, xkey);
 }
 // Slab test of a box (= the closest of its six quads): entry distance tn, or the exit tf for
 // a ray that starts inside (what the quads give). A ray leaving one of the box's faces

@@ -841,10 +841,10 @@ struct StackTrav {
 #ifndef RT_SHADE_BATCH_GLOBAL  // the same for trees in HBM (speculative traversal): C4 stand-in 413.6 ms/frame
 #define RT_SHADE_BATCH_GLOBAL 48  // never pausing, 415.2 / 370.8 / 363.8 / 362.5 / 368.4 / 379.6 at 16/32/40/48/56/60
 #endif
-#ifndef RT_WIDE_WAVES_F64  // fp64 rays over the wide tree (round 3): tree in LDS / in HBM
-#define RT_WIDE_WAVES_F64 1
+#ifndef RT_WIDE_WAVES_F64  // fp64 rays over the wide tree (round 3), tree in LDS (C3 fp64, ms/frame: 2 or 3 waves
+#define RT_WIDE_WAVES_F64 4  // 99, 4 waves 90.2)
 #endif
-#ifndef RT_WIDE_WAVES_GLOBAL_F64
+#ifndef RT_WIDE_WAVES_GLOBAL_F64  // tree in HBM (C4 fp64: 3 waves 599.8, 4: 555.0, 5: 567.3)
 #define RT_WIDE_WAVES_GLOBAL_F64 4
 #endif
 template <class R, bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN, int QN = 0>

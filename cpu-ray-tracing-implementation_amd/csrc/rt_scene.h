@@ -79,7 +79,6 @@ static_assert(3 * kMaxChain <= 14, "an instance chain must fit one LinRec");
 // decides exact-t ties.
 //   FlatQuadT, group A (plane axis): U < W are the two other axes,
 //     alpha = (o_U + t d_U - lo_u) * inv_u, beta = (o_W + t d_W - lo_w) * inv_w (signed inv);
-//   groups are padded to an even count with records whose plane is NaN (never hit).
 //   nm (both records) = what shade needs of the hit: material | A << 28 | (n_A < 0) << 31, the
 //   quad's outward normal being +-e_A exactly (translations leave normals alone).
 template <class R>
@@ -307,7 +306,7 @@ struct SceneHeader {
   uint64_t bytes;
   uint32_t n_linear;  // 0: no linear program (use the BVH traversal)
   uint32_t n_flat_box;          // flat program: boxes
-  uint32_t n_flat_quad[3];      // flat program: quads per plane axis (even counts)
+  uint32_t n_flat_quad[3];      // flat program: quads per plane axis
   uint32_t has_flat;            // 1: the flat program replaces the linear program (RT_TRAV_AUTO)
   uint64_t off_flat_quad, off_flat_box;
   uint32_t n_quads, n_spheres, n_tris, n_volumes, n_nodes, n_refs, n_mats, n_texs;

@@ -958,14 +958,6 @@ bool Compiler::flat_program(const std::vector<uint32_t>& lin, std::vector<FlatQu
   }
   quads.clear();
   for (int a = 0; a < 3; a++) {
-    if (grp[a].size() % 2) {  // pad to pairs: a NaN plane never hits
-      FlatQuadT<double> pad{};
-      pad.nm = (uint32_t)a << 28;
-      pad.plane = std::numeric_limits<double>::quiet_NaN();
-      pad.e = kNoHit;
-      pad.inst = -2;
-      grp[a].push_back(pad);
-    }
     nq[a] = (uint32_t)grp[a].size();
     quads.insert(quads.end(), grp[a].begin(), grp[a].end());
   }

@@ -71,7 +71,7 @@ def test_scene_check_config_scenes(name, quads, spheres, linear, flat):
     # the fp32 wide BVH: only RTOW (a bvh_node of world-level spheres) gets one
     if name == "rtow":
         assert info.wide_kinds == 1 and 0 < info.wide_nodes < 339 and 1 <= info.wide_stack <= 32
-        assert info.wide_prim_words == 2 * 339  # [c1, entry] [dc, r] per sphere
+        assert info.wide_prim_words == 2 * 339 + 2  # [c1, entry] [dc, r] per sphere, then two padding words
         assert info.wide_big == 1  # the r = 1000 ground, tested before the tree
     else:
         assert info.wide_nodes == 0 and info.wide_kinds == 0
