@@ -21,6 +21,12 @@ namespace rtd {
 #ifndef RT_WIDE_SPEC  // wide BVH in HBM: speculative while-while traversal (trace_wide)
 #define RT_WIDE_SPEC 1
 #endif
+#ifndef RT_WIDE_FMA  // fp64 rays over the wide BVH: octant-ordered planes, one fma per plane distance
+#define RT_WIDE_FMA 1
+#endif
+#ifndef RT_WIDE_OCT32  // fp32 rays over the wide BVH: octant-ordered planes, (p - o) * inv (C3 fp32 60.87 ->
+#define RT_WIDE_OCT32 1  // 57.22 ms/frame, C4 351.9 -> 341.6)
+#endif
 #ifndef RT_WIDE_PREFETCH  // a triangle's words loaded with the record's first word (C4 358.9 -> 357.2 ms)
 #define RT_WIDE_PREFETCH 1
 #endif
@@ -535,6 +541,68 @@ __device__ __forceinline__ T ld_uniform(const T* p, uint32_t i) {
   return p[i];  // host pass of a device function: never executed
 #endif
 }
+// A wave-uniform record into SGPRs by explicit scalar loads (s_load_dwordx16 / x8 / x4, one s_waitcnt for
+// all of them). ld_uniform's constant-address-space load is turned back into per-lane vector loads
+// (global_load with a zero VGPR offset) in the large persistent kernels (round 3: the flat program's
+// record pairs, boxes and the linear program's records), each a VMEM issue and an L1 round trip.
+#ifndef RT_SCALAR_ASM
+#define RT_SCALAR_ASM 1
+#endif
+typedef uint32_t SRegs16 __attribute__((ext_vector_type(16)));
+typedef uint32_t SRegs8 __attribute__((ext_vector_type(8)));
+typedef uint32_t SRegs4 __attribute__((ext_vector_type(4)));
+template <class T>
+__device__ __forceinline__ T ld_scalar(const T* p) {
+#if defined(__HIP_DEVICE_COMPILE__) && RT_SCALAR_ASM
+  constexpr uint32_t n = sizeof(T) / 4;
+  static_assert(sizeof(T) % 16 == 0 && n <= 32, "ld_scalar: 16-byte multiples up to 128 bytes");
+  T t;
+  if constexpr (n == 32) {
+    SRegs16 a, b;
+    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&s"(a), "=&s"(b) : "s"(p));
+    __builtin_memcpy((char*)&t, &a, 64);
+    __builtin_memcpy((char*)&t + 64, &b, 64);
+  } else if constexpr (n == 24) {
+    SRegs16 a;
+    SRegs8 b;
+    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx8 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&s"(a), "=&s"(b) : "s"(p));
+    __builtin_memcpy((char*)&t, &a, 64);
+    __builtin_memcpy((char*)&t + 64, &b, 32);
+  } else if constexpr (n == 20) {
+    SRegs16 a;
+    SRegs4 b;
+    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx4 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&s"(a), "=&s"(b) : "s"(p));
+    __builtin_memcpy((char*)&t, &a, 64);
+    __builtin_memcpy((char*)&t + 64, &b, 16);
+  } else if constexpr (n == 16) {
+    SRegs16 a;
+    asm volatile("s_load_dwordx16 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=&s"(a) : "s"(p));
+    __builtin_memcpy((char*)&t, &a, 64);
+  } else if constexpr (n == 12) {
+    SRegs8 a;
+    SRegs4 b;
+    asm volatile("s_load_dwordx8 %0, %2, 0x0\n\ts_load_dwordx4 %1, %2, 0x20\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&s"(a), "=&s"(b) : "s"(p));
+    __builtin_memcpy((char*)&t, &a, 32);
+    __builtin_memcpy((char*)&t + 32, &b, 16);
+  } else if constexpr (n == 8) {
+    SRegs8 a;
+    asm volatile("s_load_dwordx8 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=&s"(a) : "s"(p));
+    __builtin_memcpy((char*)&t, &a, 32);
+  } else {
+    static_assert(n == 4, "ld_scalar size");
+    SRegs4 a;
+    asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=&s"(a) : "s"(p));
+    __builtin_memcpy((char*)&t, &a, 16);
+  }
+  return t;
+#else
+  return ld_uniform(p, 0);
+#endif
+}
 // ld_uniform at the point of use: the index is an opaque zero, so the scalar load cannot be
 // hoisted out of the path loop. Loop-invariant uniforms (the light, the camera) hoisted to the
 // kernel entry outlive the SGPR budget and are spilled into VGPR lanes, and every use then costs
@@ -860,6 +928,27 @@ __device__ void trace(const DevScene<R>& sc, const Node<R>* nodes, V<R> wo, V<R>
 // LDS copy of a node: 144-byte stride (36 dwords), so the 16 lanes of a ds_read_b128 group that
 // read 16 consecutive nodes hit 16 distinct 4-bank windows (a 128-byte stride gives 2).
 constexpr uint32_t kWNodeLdsStride = 144;
+#ifdef RT_SECTION_CLOCKS
+// development build (scripts/dev_wide_stats.py): wave-level counts of the wide kernels, per block
+// in LDS, added to g_wide_stats at the end: [0] node-loop iterations, [1] lanes in them, [2]
+// primitive tests (wave iterations), [3] lanes in them, [4] shade calls, [5] lanes in them,
+// [6] trace clocks, [7] shade clocks (both per wave, summed)
+__device__ unsigned long long g_wide_stats[8];
+__device__ __forceinline__ unsigned long long* wide_stats_lds() {
+  __shared__ unsigned long long ws[8];
+  return ws;
+}
+__device__ __forceinline__ void wide_stat(int k) {  // one wave-level event with the calling lanes
+  const uint64_t m = __ballot(1);
+  if (__lane_id() == (uint32_t)__ffsll((unsigned long long)m) - 1) {
+    atomicAdd(wide_stats_lds() + k, 1ull);
+    atomicAdd(wide_stats_lds() + k + 1, (unsigned long long)__popcll(m));
+  }
+}
+#define RT_WIDE_STAT(k) wide_stat(k)
+#else
+#define RT_WIDE_STAT(k)
+#endif
 // The traversal of one ray is resumable: (cur, sp, tmax, e_best) and the LDS stack are its whole
 // state. It returns true once the ray is finished, or false -- the ray paused -- when `pause` of
 // the wave's lanes that entered are finished and waiting: the persistent kernel then shades those
@@ -1013,26 +1102,86 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
     if (LDSN || sp < (int)kWideLdsStack) return stk[sp * BLOCK];
     return sc.wide_spill[(uint32_t)(sp - (int)kWideLdsStack) * sc.spill_lanes + lane];
   };
-  auto slab = [&](float lx, float ly, float lz, float hx, float hy, float hz, uint32_t c) {
-    const float tx0 = (lx - o.x) * inv.x, tx1 = (hx - o.x) * inv.x;
-    const float ty0 = (ly - o.y) * inv.y, ty1 = (hy - o.y) * inv.y;
-    const float tz0 = (lz - o.z) * inv.z, tz1 = (hz - o.z) * inv.z;
-    float tn, tf;
-    if constexpr (F64) {
-      tn = fmaxf(fmaxf(fminf(tx0, tx1) - wx, fminf(ty0, ty1) - wy), fmaxf(fminf(tz0, tz1) - wz, tmin_box));
-      tf = fminf(fminf(fmaxf(tx0, tx1) + wx, fmaxf(ty0, ty1) + wy), fminf(fmaxf(tz0, tz1) + wz, (float)tmax)) *
-           Num<float>::box_slack();
-    } else {
-      tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin_box));
-      tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), (float)tmax)) *
-           Num<float>::box_slack();
-    }
+  // Node tests (round 3). Octant-ordered: per axis the near plane (lo for a positive direction, hi
+  // for a negative one) is read from its byte offset in the node (lo_a at 16a, hi_a at 48 + 16a), so a
+  // child needs no min/max per axis. fp64 rays (RT_WIDE_FMA): each plane distance is one fma,
+  // p * inv + c with c = -o * inv per ray; c carries the rounding of o * inv: the near constant is
+  // lowered and the far one raised by |o * inv| 2^-22 (> twice the two roundings involved) plus the
+  // widening w of the ray's rounding to float, the fma's own rounding being covered, like the
+  // subtraction's, by box_slack. A direction component of 0 gives inv = inf: its planes' distances
+  // are NaN or -inf, which the IEEE min/max ignore (no culling on that axis, as before). The six
+  // constants cost the fp32 kernels, at their tighter register budgets, more spills than the fmas
+  // save (C4 fp32 351 -> 460 ms/frame; fp64 C3 89.8 -> 81.7, C4 561 -> 545), so fp32 keeps
+  // (p - o) * inv, octant-ordered (RT_WIDE_OCT32: C3 fp32 60.9 -> 57.2, C4 351.9 -> 341.6).
+  constexpr bool kFma = F64 && RT_WIDE_FMA, kOct = kFma || (!F64 && RT_WIDE_OCT32);
+  [[maybe_unused]] const uint32_t onx = (__float_as_uint(inv.x) >> 31) * 48u, ony = 16u + (__float_as_uint(inv.y) >> 31) * 48u,
+                 onz = 32u + (__float_as_uint(inv.z) >> 31) * 48u;
+  [[maybe_unused]] float cnx = 0.f, cny = 0.f, cnz = 0.f, cfx = 0.f, cfy = 0.f, cfz = 0.f;
+  if constexpr (kFma) {
+    auto cpair = [](float oa, float ia, float wa, float& cn, float& cf) {
+      const float oi = oa * ia;
+      const float ea = fmaf(fabsf(oi), 2.384185791015625e-07f, wa);
+      cn = -oi - ea;
+      cf = -oi + ea;
+    };
+    cpair(o.x, inv.x, wx, cnx, cfx);
+    cpair(o.y, inv.y, wy, cny, cfy);
+    cpair(o.z, inv.z, wz, cnz, cfz);
+  }
+  // the four children's sort keys (bits(t_near) with the slot in the low 2 bits; 0xFFFFFFFF: missed)
+  // of the float node at nb (LDS or HBM)
+  auto node_keys = [&](const unsigned char* nb, uint32_t& k0, uint32_t& k1, uint32_t& k2, uint32_t& k3) {
+    const float tmx = (float)tmax;
     // tn >= tmin > 0: the bit pattern orders like the value; the low 2 bits carry the slot
-    return tn <= tf ? ((__float_as_uint(tn) & ~3u) | c) : 0xFFFFFFFFu;
+    auto keyof = [](float tn, float tf, uint32_t c) {
+      return tn <= tf ? ((__float_as_uint(tn) & ~3u) | c) : 0xFFFFFFFFu;
+    };
+    if constexpr (kOct) {
+      const float4 nx = *(const float4*)(nb + onx), ny = *(const float4*)(nb + ony), nz = *(const float4*)(nb + onz);
+      const float4 fx = *(const float4*)(nb + (48u - onx)), fy = *(const float4*)(nb + (80u - ony)),
+                   fz = *(const float4*)(nb + (112u - onz));
+      auto key = [&](float px, float py, float pz, float qx, float qy, float qz, uint32_t c) {
+        float tn, tf;
+        if constexpr (kFma) {
+          tn = fmaxf(fmaxf(fmaf(px, inv.x, cnx), fmaf(py, inv.y, cny)), fmaxf(fmaf(pz, inv.z, cnz), tmin_box));
+          tf = fminf(fminf(fmaf(qx, inv.x, cfx), fmaf(qy, inv.y, cfy)), fminf(fmaf(qz, inv.z, cfz), tmx));
+        } else {
+          tn = fmaxf(fmaxf((px - o.x) * inv.x, (py - o.y) * inv.y), fmaxf((pz - o.z) * inv.z, tmin_box));
+          tf = fminf(fminf((qx - o.x) * inv.x, (qy - o.y) * inv.y), fminf((qz - o.z) * inv.z, tmx));
+        }
+        return keyof(tn, tf * Num<float>::box_slack(), c);
+      };
+      k0 = key(nx.x, ny.x, nz.x, fx.x, fy.x, fz.x, 0u);
+      k1 = key(nx.y, ny.y, nz.y, fx.y, fy.y, fz.y, 1u);
+      k2 = key(nx.z, ny.z, nz.z, fx.z, fy.z, fz.z, 2u);
+      k3 = key(nx.w, ny.w, nz.w, fx.w, fy.w, fz.w, 3u);
+    } else {
+      const float4* nd = (const float4*)nb;
+      const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
+      auto slab = [&](float lx, float ly, float lz, float hx, float hy, float hz, uint32_t c) {
+        const float tx0 = (lx - o.x) * inv.x, tx1 = (hx - o.x) * inv.x;
+        const float ty0 = (ly - o.y) * inv.y, ty1 = (hy - o.y) * inv.y;
+        const float tz0 = (lz - o.z) * inv.z, tz1 = (hz - o.z) * inv.z;
+        float tn, tf;
+        if constexpr (F64) {
+          tn = fmaxf(fmaxf(fminf(tx0, tx1) - wx, fminf(ty0, ty1) - wy), fmaxf(fminf(tz0, tz1) - wz, tmin_box));
+          tf = fminf(fminf(fmaxf(tx0, tx1) + wx, fmaxf(ty0, ty1) + wy), fminf(fmaxf(tz0, tz1) + wz, tmx));
+        } else {
+          tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin_box));
+          tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmx));
+        }
+        return keyof(tn, tf * Num<float>::box_slack(), c);
+      };
+      k0 = slab(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, 0u);
+      k1 = slab(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, 1u);
+      k2 = slab(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, 2u);
+      k3 = slab(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, 3u);
+    }
   };
   // the primitives of a leaf (or of the head list), their records from word w on
   auto test_prims = [&](uint32_t w, uint32_t count) {
     for (uint32_t n = count; n > 0; n--) {
+      RT_WIDE_STAT(2);
       const WW h = prims[w];
       // a kernel with triangles loads a record's next two words with its first (the word stream is
       // padded, rt_scene.h), so a triangle costs one memory latency, not two: its kind is in word 0
@@ -1082,6 +1231,7 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
   for (;;) {
     uint32_t leaf = 0u;  // the postponed leaf (a leaf code is never 0)
     while (have) {
+      RT_WIDE_STAT(0);
       if (cur & kLeafBit) {
         if (leaf) break;  // a second leaf: test the first, come back with this one
         leaf = cur;
@@ -1113,12 +1263,8 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
         if constexpr (QN == 4) {  // a quantised 4-wide node (HBM trees)
           wideq4_keys((const WNodeQ4*)sc.wnodesq + cur, o, inv, tmin, tmax, k0, k1, k2, k3, cc);
         } else {
-          const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
           if constexpr (!LDSN) cc = *(const uint4*)(nd + 6);
-          k0 = slab(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, 0u);
-          k1 = slab(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, 1u);
-          k2 = slab(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, 2u);
-          k3 = slab(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, 3u);
+          node_keys((const unsigned char*)nd, k0, k1, k2, k3);
         }
         auto child = [&](uint32_t k) -> uint32_t {
           if constexpr (LDSN) {
@@ -1173,8 +1319,8 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
   } else {
   for (;;) {
     while (!(cur & kLeafBit)) {  // inner nodes until this lane holds a leaf (while-while)
+      RT_WIDE_STAT(0);
       const float4* nd = LDSN ? (const float4*)(lds_nodes + (cur << 4)) : (const float4*)(sc.wnodes + cur);
-      const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
       // LDS tree: a child's code is loaded when it is pushed (loading all four with the boxes keeps them
       // live through the slab tests and the sort, which spilled: C3 76.4 -> 81.5 ms/frame). Tree in HBM:
       // all four come with the boxes, one latency instead of one per push (C4 462 -> 421 ms/frame).
@@ -1188,10 +1334,8 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
           return sl == 0 ? cc.x : (sl == 1 ? cc.y : (sl == 2 ? cc.z : cc.w));
         }
       };
-      uint32_t k0 = slab(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, 0u);
-      uint32_t k1 = slab(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, 1u);
-      uint32_t k2 = slab(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, 2u);
-      uint32_t k3 = slab(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, 3u);
+      uint32_t k0, k1, k2, k3;
+      node_keys((const unsigned char*)nd, k0, k1, k2, k3);
 #define RT_CS(a, b)                 \
   {                                 \
     const uint32_t lo_ = min(a, b); \
@@ -1254,7 +1398,7 @@ __device__ __forceinline__ void trace_linear(const DevScene<R>& sc, V<R> wo, V<R
   i_best = -1;
   const uint32_t n = sc.n_linear;
   for (uint32_t k = 0; k < n; k++) {
-    const LinRec<R> rec = ld_uniform(sc.lin, k);  // the whole record into SGPRs at once
+    const LinRec<R> rec = ld_scalar(sc.lin + k);  // the whole record into SGPRs at once
     const uint32_t op = rec.op;
     const uint32_t ty = etype(op), idx = epay(op);
     R th;
@@ -1361,11 +1505,11 @@ __device__ __forceinline__ void flat_quads(const FlatQuadT<R>* q, uint32_t n, in
   // to pairs with never-hit records -- Cornell's y and z groups had one each, 2 of 8 quad tests)
 #pragma unroll 1
   for (uint32_t k = 0; k + 1 < n; k += 2) {
-    const FlatQuad2<R> r = ld_uniform(reinterpret_cast<const FlatQuad2<R>*>(q + k), 0);
+    const FlatQuad2<R> r = ld_scalar(reinterpret_cast<const FlatQuad2<R>*>(q + k));
     flat_quad_test<A>(r.a, base + (int32_t)k, o, d, inv, tmin, tmax, best, xkey);
     flat_quad_test<A>(r.b, base + (int32_t)k + 1, o, d, inv, tmin, tmax, best, xkey);
   }
-  if (n & 1u) flat_quad_test<A>(ld_uniform(q, n - 1), base + (int32_t)(n - 1), o, d, inv, tmin, tmax, best, xkey);
+  if (n & 1u) flat_quad_test<A>(ld_scalar(q + (n - 1)), base + (int32_t)(n - 1), o, d, inv, tmin, tmax, best, xkey);
 }
 // Slab test of a box (= the closest of its six quads): entry distance tn, or the exit tf for
 // a ray that starts inside (what the quads give). A ray leaving one of the box's faces
@@ -1408,7 +1552,7 @@ __device__ __forceinline__ void trace_flat(const DevScene<R>& sc, V<R> o, V<R> d
   flat_quads<2>(sc.flatq + n0 + n1, n2, (int32_t)(n0 + n1), o, d, inv, tmin, tmax, best, xkey);
 #pragma unroll 1
   for (uint32_t k = 0; k < sc.n_flatb; k++) {
-    const FlatBoxT<R> b = ld_uniform(sc.flatb, k);
+    const FlatBoxT<R> b = ld_scalar(sc.flatb + k);
     const Slab<R> s = flat_slab(b, o, inv, tmin, excl_i, xf);
     const bool h = (s.tn <= s.tf) & (s.th >= tmin) & (s.th <= tmax);
     tmax = h ? s.th : tmax;

@@ -995,6 +995,10 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
   [[maybe_unused]] void* wstk = nullptr;  // the wide traversal's lane stack (uint16 or uint32 entries)
   if constexpr (Trav::kWide) {
     extern __shared__ uint4 dyn_lds[];
+#ifdef RT_SECTION_CLOCKS
+    if (threadIdx.x < 8) wide_stats_lds()[threadIdx.x] = 0;
+    __syncthreads();
+#endif
     wstk = Trav::fill(p.sc, dyn_lds) + threadIdx.x;
     trav_nodes = (const Node<R>*)dyn_lds;
   }
@@ -1030,7 +1034,15 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
 #else
         const Params<R>& q = p;  // (reloading q per segment as below: C3 1.5 % slower at 6 waves)
 #endif
+#ifdef RT_SECTION_CLOCKS
+        const uint64_t c0 = clock64();
+        const bool fin = Trav::steps(q.sc, trav_nodes, s, (StackT*)wstk, ry);
+        if (__lane_id() == (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1)
+          atomicAdd(wide_stats_lds() + 6, (unsigned long long)(clock64() - c0));
+        if (!fin) continue;
+#else
         if (!Trav::steps(q.sc, trav_nodes, s, (StackT*)wstk, ry)) continue;
+#endif
         if (++segs > q.seg_cap) {  // cannot happen: every segment advances a bounce-capped path
           atomicOr(q.fault, 1u);
           break;
@@ -1038,7 +1050,16 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
         const R t = ry.tmax;
         const uint32_t e = ry.e;
         ry = WideRayT<R>{root, 0, Num<R>::inf(), kNoHit, 1u};
+#ifdef RT_SECTION_CLOCKS
+        RT_WIDE_STAT(4);
+        const uint64_t c1 = clock64();
+        const bool more = shade<R, CAMX, false>(q, s, t, e, -1, 0);
+        if (__lane_id() == (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1)
+          atomicAdd(wide_stats_lds() + 7, (unsigned long long)(clock64() - c1));
+        if (!more) break;
+#else
         if (!shade<R, CAMX, false>(q, s, t, e, -1, 0)) break;
+#endif
       }
     } else {
 #if RT_PARAM_RELOAD
@@ -1078,6 +1099,9 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
     uint64_t c = (uint64_t)wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3];
     if (c) atomicAdd(&p.seg_shards[blockIdx.x % kSegShards], (unsigned long long)c);
   }
+#ifdef RT_SECTION_CLOCKS
+  if (Trav::kWide && threadIdx.x < 8) atomicAdd(&g_wide_stats[threadIdx.x], wide_stats_lds()[threadIdx.x]);
+#endif
 }
 template <class R, class Trav, bool CAMX>
 __global__ __launch_bounds__(kBlock) void k_persist(Params<R> p) {
@@ -2001,9 +2025,16 @@ rt_status rt_set_timing(rt_context* c, int32_t enable) {
 void rt_dev_section_clocks(unsigned long long out[7]) {
   hipMemcpyFromSymbol(out, HIP_SYMBOL(g_section_clocks), sizeof(unsigned long long) * 4);
   hipMemcpyFromSymbol(out + 4, HIP_SYMBOL(rtd::g_trace_totals), sizeof(unsigned long long) * 3);
-  unsigned long long z[4] = {0, 0, 0, 0};
+  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   hipMemcpyToSymbol(HIP_SYMBOL(g_section_clocks), z, sizeof(z));
   hipMemcpyToSymbol(HIP_SYMBOL(rtd::g_trace_totals), z, sizeof(unsigned long long) * 3);
+}
+// the wide kernels' wave-level counts (rt_device.h g_wide_stats), read and cleared
+void rt_dev_wide_stats(unsigned long long out[8]) {
+  hipDeviceSynchronize();
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(rtd::g_wide_stats), sizeof(unsigned long long) * 8);
+  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  hipMemcpyToSymbol(HIP_SYMBOL(rtd::g_wide_stats), z, sizeof(z));
 }
 #endif
 
