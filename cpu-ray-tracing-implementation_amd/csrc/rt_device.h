@@ -932,10 +932,10 @@ constexpr uint32_t kWNodeLdsStride = 144;
 // development build (scripts/dev_wide_stats.py): wave-level counts of the wide kernels, per block
 // in LDS, added to g_wide_stats at the end: [0] node-loop iterations, [1] lanes in them, [2]
 // primitive tests (wave iterations), [3] lanes in them, [4] shade calls, [5] lanes in them,
-// [6] trace clocks, [7] shade clocks (both per wave, summed)
-__device__ unsigned long long g_wide_stats[8];
+// [6] trace clocks, [7] shade clocks (both per wave, summed), [8] finished samples, [9] lanes in them
+__device__ unsigned long long g_wide_stats[10];
 __device__ __forceinline__ unsigned long long* wide_stats_lds() {
-  __shared__ unsigned long long ws[8];
+  __shared__ unsigned long long ws[10];
   return ws;
 }
 __device__ __forceinline__ void wide_stat(int k) {  // one wave-level event with the calling lanes
@@ -1130,16 +1130,21 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
   }
   // the four children's sort keys (bits(t_near) with the slot in the low 2 bits; 0xFFFFFFFF: missed)
   // of the float node at nb (LDS or HBM)
-  auto node_keys = [&](const unsigned char* nb, uint32_t& k0, uint32_t& k1, uint32_t& k2, uint32_t& k3) {
+  // (a tree in HBM is addressed as its base plus a 32-bit byte offset, so each load is one global_load
+  // with the base in SGPRs and the offset in one VGPR, not a 64-bit address per plane)
+  const unsigned char* nbase = LDSN ? lds_nodes : (const unsigned char*)sc.wnodes;
+  auto node_off = [](uint32_t c) -> uint32_t { return LDSN ? (c << 4) : c * (uint32_t)sizeof(WNode); };
+  auto node_keys = [&](uint32_t nof, uint32_t& k0, uint32_t& k1, uint32_t& k2, uint32_t& k3) {
     const float tmx = (float)tmax;
     // tn >= tmin > 0: the bit pattern orders like the value; the low 2 bits carry the slot
     auto keyof = [](float tn, float tf, uint32_t c) {
       return tn <= tf ? ((__float_as_uint(tn) & ~3u) | c) : 0xFFFFFFFFu;
     };
     if constexpr (kOct) {
-      const float4 nx = *(const float4*)(nb + onx), ny = *(const float4*)(nb + ony), nz = *(const float4*)(nb + onz);
-      const float4 fx = *(const float4*)(nb + (48u - onx)), fy = *(const float4*)(nb + (80u - ony)),
-                   fz = *(const float4*)(nb + (112u - onz));
+      const float4 nx = *(const float4*)(nbase + (nof + onx)), ny = *(const float4*)(nbase + (nof + ony)),
+                   nz = *(const float4*)(nbase + (nof + onz));
+      const float4 fx = *(const float4*)(nbase + (nof + (48u - onx))), fy = *(const float4*)(nbase + (nof + (80u - ony))),
+                   fz = *(const float4*)(nbase + (nof + (112u - onz)));
       auto key = [&](float px, float py, float pz, float qx, float qy, float qz, uint32_t c) {
         float tn, tf;
         if constexpr (kFma) {
@@ -1156,7 +1161,7 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
       k2 = key(nx.z, ny.z, nz.z, fx.z, fy.z, fz.z, 2u);
       k3 = key(nx.w, ny.w, nz.w, fx.w, fy.w, fz.w, 3u);
     } else {
-      const float4* nd = (const float4*)nb;
+      const float4* nd = (const float4*)(nbase + nof);
       const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
       auto slab = [&](float lx, float ly, float lz, float hx, float hy, float hz, uint32_t c) {
         const float tx0 = (lx - o.x) * inv.x, tx1 = (hx - o.x) * inv.x;
@@ -1179,32 +1184,34 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
     }
   };
   // the primitives of a leaf (or of the head list), their records from word w on
+  // a primitive word by 32-bit byte offset from the base (one VGPR of address; see node_keys)
+  auto pw = [&](uint32_t k) -> WW { return *(const WW*)((const unsigned char*)prims + k * (uint32_t)sizeof(WW)); };
   auto test_prims = [&](uint32_t w, uint32_t count) {
     for (uint32_t n = count; n > 0; n--) {
       RT_WIDE_STAT(2);
-      const WW h = prims[w];
+      const WW h = pw(w);
       // a kernel with triangles loads a record's next two words with its first (the word stream is
       // padded, rt_scene.h), so a triangle costs one memory latency, not two: its kind is in word 0
       [[maybe_unused]] WW a1{}, a2{};
       constexpr bool PF = TRI && RT_WIDE_PREFETCH;
       if constexpr (PF) {
-        a1 = prims[w + 1];
-        a2 = prims[w + 2];
+        a1 = pw(w + 1);
+        a2 = pw(w + 2);
       }
       const uint32_t e = wentry(h);
       const uint32_t ty = etype(e);
       R th;
       bool hit = false;
       if (SPH && (!(TRI || QUAD) || ty == E_SPHERE)) {
-        const WW b = PF ? a1 : prims[w + 1];
+        const WW b = PF ? a1 : pw(w + 1);
         w += 2;
         hit = sphere_test(mkv(h.x, h.y, h.z), mkv(b.x, b.y, b.z), b.w, MOV, ro, rd, time, tmin, tmax, e == excl_e, th);
       } else if (TRI && (!QUAD || ty == E_TRI)) {
-        const WW a = PF ? a1 : prims[w + 1], b = PF ? a2 : prims[w + 2];
+        const WW a = PF ? a1 : pw(w + 1), b = PF ? a2 : pw(w + 2);
         w += 3;
         hit = e != excl_e && tri_test(mkv(h.x, h.y, h.z), mkv(a.x, a.y, a.z), mkv(b.x, b.y, b.z), ro, rd, tmin, tmax, th);
       } else if (QUAD) {
-        const WW nD = PF ? a1 : prims[w + 1], qa = PF ? a2 : prims[w + 2], qb = prims[w + 3];
+        const WW nD = PF ? a1 : pw(w + 1), qa = PF ? a2 : pw(w + 2), qb = pw(w + 3);
         w += 4;
         hit = e != excl_e && quad_test(mkv(nD.x, nD.y, nD.z), nD.w, mkv(h.x, h.y, h.z), mkv(qa.x, qa.y, qa.z),
                                        mkv(qb.x, qb.y, qb.z), ro, rd, tmin, tmax, th);
@@ -1257,18 +1264,18 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
           cur = wide8_child(k[0], c0, c1);
         }
       } else {
-        const float4* nd = LDSN ? (const float4*)(lds_nodes + (cur << 4)) : (const float4*)(sc.wnodes + cur);
+        const uint32_t nof = node_off(cur);
         uint4 cc{};
         uint32_t k0, k1, k2, k3;
         if constexpr (QN == 4) {  // a quantised 4-wide node (HBM trees)
           wideq4_keys((const WNodeQ4*)sc.wnodesq + cur, o, inv, tmin, tmax, k0, k1, k2, k3, cc);
         } else {
-          if constexpr (!LDSN) cc = *(const uint4*)(nd + 6);
-          node_keys((const unsigned char*)nd, k0, k1, k2, k3);
+          if constexpr (!LDSN) cc = *(const uint4*)(nbase + (nof + 96u));
+          node_keys(nof, k0, k1, k2, k3);
         }
         auto child = [&](uint32_t k) -> uint32_t {
           if constexpr (LDSN) {
-            return ((const uint16_t*)(nd + 6))[k & 3u];
+            return ((const uint16_t*)(nbase + (nof + 96u)))[k & 3u];
           } else {
             const uint32_t sl = k & 3u;
             return sl == 0 ? cc.x : (sl == 1 ? cc.y : (sl == 2 ? cc.z : cc.w));
@@ -1320,22 +1327,22 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
   for (;;) {
     while (!(cur & kLeafBit)) {  // inner nodes until this lane holds a leaf (while-while)
       RT_WIDE_STAT(0);
-      const float4* nd = LDSN ? (const float4*)(lds_nodes + (cur << 4)) : (const float4*)(sc.wnodes + cur);
+      const uint32_t nof = node_off(cur);
       // LDS tree: a child's code is loaded when it is pushed (loading all four with the boxes keeps them
       // live through the slab tests and the sort, which spilled: C3 76.4 -> 81.5 ms/frame). Tree in HBM:
       // all four come with the boxes, one latency instead of one per push (C4 462 -> 421 ms/frame).
       uint4 cc{};
-      if constexpr (!LDSN) cc = *(const uint4*)(nd + 6);
+      if constexpr (!LDSN) cc = *(const uint4*)(nbase + (nof + 96u));
       auto child = [&](uint32_t k) -> uint32_t {
         if constexpr (LDSN) {
-          return ((const uint16_t*)(nd + 6))[k & 3u];
+          return ((const uint16_t*)(nbase + (nof + 96u)))[k & 3u];
         } else {
           const uint32_t sl = k & 3u;
           return sl == 0 ? cc.x : (sl == 1 ? cc.y : (sl == 2 ? cc.z : cc.w));
         }
       };
       uint32_t k0, k1, k2, k3;
-      node_keys((const unsigned char*)nd, k0, k1, k2, k3);
+      node_keys(nof, k0, k1, k2, k3);
 #define RT_CS(a, b)                 \
   {                                 \
     const uint32_t lo_ = min(a, b); \

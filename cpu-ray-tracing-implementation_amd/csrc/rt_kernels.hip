@@ -724,6 +724,7 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
     return true;
   }
   // the sample is finished (camera.h:167): add it to the item's running sum
+  RT_WIDE_STAT(8);
   const V<R> acc = s.acc() + s.rad;
   const uint32_t sample = s.sample() + 1;
   s.set_sample(sample);
@@ -993,12 +994,12 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
   uint32_t* stk_lane = stk.v + threadIdx.x;
   const Node<R>* trav_nodes = lds_nodes;
   [[maybe_unused]] void* wstk = nullptr;  // the wide traversal's lane stack (uint16 or uint32 entries)
+#ifdef RT_SECTION_CLOCKS
+  if (threadIdx.x < 10) wide_stats_lds()[threadIdx.x] = 0;
+  __syncthreads();
+#endif
   if constexpr (Trav::kWide) {
     extern __shared__ uint4 dyn_lds[];
-#ifdef RT_SECTION_CLOCKS
-    if (threadIdx.x < 8) wide_stats_lds()[threadIdx.x] = 0;
-    __syncthreads();
-#endif
     wstk = Trav::fill(p.sc, dyn_lds) + threadIdx.x;
     trav_nodes = (const Node<R>*)dyn_lds;
   }
@@ -1082,12 +1083,26 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
         R t;
         uint32_t e, nm = 0;
         int32_t inst;
+#ifdef RT_SECTION_CLOCKS
+        RT_WIDE_STAT(0);
+        const uint64_t c0 = clock64();
+#endif
         Trav::run(q.sc, trav_nodes, s, Keys{s.ks}, stk_lane, t, e, inst, nm);
         if (++segs > q.seg_cap) {  // cannot happen: every segment advances a bounce-capped path
           atomicOr(q.fault, 1u);
           break;
         }
+#ifdef RT_SECTION_CLOCKS
+        const uint64_t c1 = clock64();
+        const bool more = shade<R, CAMX, Trav::kFlat>(q, s, t, e, inst, nm);
+        if (__lane_id() == (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1) {
+          atomicAdd(wide_stats_lds() + 6, (unsigned long long)(c1 - c0));
+          atomicAdd(wide_stats_lds() + 7, (unsigned long long)(clock64() - c1));
+        }
+        if (!more) break;
+#else
         if (!shade<R, CAMX, Trav::kFlat>(q, s, t, e, inst, nm)) break;
+#endif
       }
     }
   }
@@ -1100,7 +1115,7 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
     if (c) atomicAdd(&p.seg_shards[blockIdx.x % kSegShards], (unsigned long long)c);
   }
 #ifdef RT_SECTION_CLOCKS
-  if (Trav::kWide && threadIdx.x < 8) atomicAdd(&g_wide_stats[threadIdx.x], wide_stats_lds()[threadIdx.x]);
+  if (threadIdx.x < 10) atomicAdd(&g_wide_stats[threadIdx.x], wide_stats_lds()[threadIdx.x]);
 #endif
 }
 template <class R, class Trav, bool CAMX>
@@ -2030,11 +2045,11 @@ void rt_dev_section_clocks(unsigned long long out[7]) {
   hipMemcpyToSymbol(HIP_SYMBOL(rtd::g_trace_totals), z, sizeof(unsigned long long) * 3);
 }
 // the wide kernels' wave-level counts (rt_device.h g_wide_stats), read and cleared
-void rt_dev_wide_stats(unsigned long long out[8]) {
-  hipDeviceSynchronize();
-  hipMemcpyFromSymbol(out, HIP_SYMBOL(rtd::g_wide_stats), sizeof(unsigned long long) * 8);
-  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  hipMemcpyToSymbol(HIP_SYMBOL(rtd::g_wide_stats), z, sizeof(z));
+void rt_dev_wide_stats(unsigned long long out[10]) {
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(rtd::g_wide_stats), sizeof(unsigned long long) * 10);
+  unsigned long long z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(rtd::g_wide_stats), z, sizeof(z));
 }
 #endif
 

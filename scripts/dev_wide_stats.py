@@ -19,19 +19,21 @@ cs = plugin.ConfigScene(name, w, aspect)
 ctx = rt_amd.Context(0)
 ctx.upload(cs.desc)
 lib = abi.load()
-buf = (ctypes.c_ulonglong * 8)()
+buf = (ctypes.c_ulonglong * 10)()
 ctx.render(cs.cam, spp, depth, seed=1, precision=prec)
 lib.rt_dev_wide_stats(buf)
 ctx.reset_counters()
 ctx.render(cs.cam, spp, depth, seed=1, precision=prec)
 lib.rt_dev_wide_stats(buf)
 segs = ctx.stats().segments
-ni, nl, pi, pl, si, sl, ct, csh = list(buf)
+ni, nl, pi, pl, si, sl, ct, csh, fi, fl = list(buf)
 print(f"{cfg} {name} {w}px {spp}spp d{depth} prec={prec}: segments {segs}")
+print(f"  (flat / linear kernels: node loop = trace calls)")
 print(f"  node loop: {ni / segs * 64:.2f} wave-iter x64 per segment, lanes/iter {nl / max(ni, 1):.1f} "
       f"(lane visits/segment {nl / segs:.2f})")
 print(f"  prim tests: {pi / segs * 64:.2f} wave-iter x64 per segment, lanes/iter {pl / max(pi, 1):.1f} "
       f"(lane tests/segment {pl / segs:.2f})")
 print(f"  shade: {si / segs * 64:.2f} wave-calls x64 per segment, lanes/call {sl / max(si, 1):.1f}")
+print(f"  finished samples: {fi / segs * 64:.2f} wave-events x64 per segment, lanes/event {fl / max(fi, 1):.1f}")
 print(f"  clocks: trace {ct / (ct + csh):.3f} shade {csh / (ct + csh):.3f}; wave-cycles per segment x64: "
       f"trace {ct / segs * 64:.0f} shade {csh / segs * 64:.0f}")
