@@ -27,6 +27,9 @@ namespace rtd {
 #ifndef RT_WIDE_OCT32  // fp32 rays over the wide BVH: octant-ordered planes, (p - o) * inv (C3 fp32 60.87 ->
 #define RT_WIDE_OCT32 1  // 57.22 ms/frame, C4 351.9 -> 341.6)
 #endif
+#ifndef RT_WIDE_OFS64  // fp64 rays keep 64-bit addresses into trees in HBM (C4 fp64: 32-bit offsets 573.5 ms/frame,
+#define RT_WIDE_OFS64 1  // 64-bit 545.1; fp32 the other way round, 340.7 -> 329.1)
+#endif
 #ifndef RT_WIDE_PREFETCH  // a triangle's words loaded with the record's first word (C4 358.9 -> 357.2 ms)
 #define RT_WIDE_PREFETCH 1
 #endif
@@ -1132,9 +1135,12 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
   // of the float node at nb (LDS or HBM)
   // (a tree in HBM is addressed as its base plus a 32-bit byte offset, so each load is one global_load
   // with the base in SGPRs and the offset in one VGPR, not a 64-bit address per plane)
+  // (RT_WIDE_OFS64: the fp64 kernels keep 64-bit addresses)
+  constexpr bool kOfs = LDSN || !F64 || !RT_WIDE_OFS64;
   const unsigned char* nbase = LDSN ? lds_nodes : (const unsigned char*)sc.wnodes;
-  auto node_off = [](uint32_t c) -> uint32_t { return LDSN ? (c << 4) : c * (uint32_t)sizeof(WNode); };
-  auto node_keys = [&](uint32_t nof, uint32_t& k0, uint32_t& k1, uint32_t& k2, uint32_t& k3) {
+  using OfsT = typename std::conditional<kOfs, uint32_t, uint64_t>::type;
+  auto node_off = [](uint32_t c) -> OfsT { return LDSN ? (OfsT)(c << 4) : (OfsT)c * (OfsT)sizeof(WNode); };
+  auto node_keys = [&](OfsT nof, uint32_t& k0, uint32_t& k1, uint32_t& k2, uint32_t& k3) {
     const float tmx = (float)tmax;
     // tn >= tmin > 0: the bit pattern orders like the value; the low 2 bits carry the slot
     auto keyof = [](float tn, float tf, uint32_t c) {
@@ -1185,7 +1191,10 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
   };
   // the primitives of a leaf (or of the head list), their records from word w on
   // a primitive word by 32-bit byte offset from the base (one VGPR of address; see node_keys)
-  auto pw = [&](uint32_t k) -> WW { return *(const WW*)((const unsigned char*)prims + k * (uint32_t)sizeof(WW)); };
+  auto pw = [&](uint32_t k) -> WW {
+    if constexpr (kOfs) return *(const WW*)((const unsigned char*)prims + k * (uint32_t)sizeof(WW));
+    return prims[k];
+  };
   auto test_prims = [&](uint32_t w, uint32_t count) {
     for (uint32_t n = count; n > 0; n--) {
       RT_WIDE_STAT(2);
@@ -1264,7 +1273,7 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
           cur = wide8_child(k[0], c0, c1);
         }
       } else {
-        const uint32_t nof = node_off(cur);
+        const OfsT nof = node_off(cur);
         uint4 cc{};
         uint32_t k0, k1, k2, k3;
         if constexpr (QN == 4) {  // a quantised 4-wide node (HBM trees)
@@ -1327,7 +1336,7 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
   for (;;) {
     while (!(cur & kLeafBit)) {  // inner nodes until this lane holds a leaf (while-while)
       RT_WIDE_STAT(0);
-      const uint32_t nof = node_off(cur);
+      const OfsT nof = node_off(cur);
       // LDS tree: a child's code is loaded when it is pushed (loading all four with the boxes keeps them
       // live through the slab tests and the sort, which spilled: C3 76.4 -> 81.5 ms/frame). Tree in HBM:
       // all four come with the boxes, one latency instead of one per push (C4 462 -> 421 ms/frame).
