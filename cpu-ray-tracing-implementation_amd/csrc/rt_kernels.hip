@@ -532,14 +532,22 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
     bool front;
     int32_t mat;
     double hu = 0, hv = 0;  // hit_record u, v (EXT kernels: picture textures); 0 where the reference leaves them stale
+    [[maybe_unused]] uint32_t fA = 0;  // FLAT: n = fs e_fA
+    [[maybe_unused]] R fs = R(1);
     if constexpr (FLAT) {  // quad.h:47-50 with n = +-e_A (translate leaves it alone, hittable.h:75-82)
+      // outward = sg e_A (sg = -1 when bit 31 is set); hit_record::set_face_normal (hittable.h:26-29):
+      // dot(d, outward) < 0 is exactly sg d_A < 0, and n = front ? outward : -outward, whose zero
+      // components are -0 on a back face, as the negation gives them
       const uint32_t A = (nm >> 28) & 3u;
-      const R sg = (nm >> 31) ? R(-1) : R(1);
-      const V<R> outward = mkv(A == 0 ? sg : R(0), A == 1 ? sg : R(0), A == 2 ? sg : R(0));
+      const bool neg = (nm >> 31) != 0;
+      const R dA = A == 0 ? d.x : (A == 1 ? d.y : d.z);
       mat = (int32_t)(nm & kNmMat);
       pw = o + t * d;
-      front = dot(d, outward) < R(0);  // hit_record::set_face_normal (hittable.h:26-29)
-      n = front ? outward : -outward;
+      front = neg ? dA > R(0) : dA < R(0);
+      fA = A;
+      fs = front != neg ? R(1) : R(-1);
+      const R z = front ? R(0) : -R(0);
+      n = mkv(A == 0 ? fs : z, A == 1 ? fs : z, A == 2 ? fs : z);
     } else if (ty == E_VOLUME) {  // volumne.h:40-44
       pw = o + t * d;
       n = mkv(R(1), R(0), R(0));
@@ -675,15 +683,33 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
         const bool iso = m.kind == M_ISOTROPIC;
         const R iso_pdf = R(1) / (R(4) * Num<R>::pi());
         Onb<R> b;
-        if (!iso) b = FLAT ? make_onb_axis(n) : make_onb(n);
+        if (!FLAT && !iso) b = make_onb(n);
+        // FLAT: n = fs e_A, so make_onb_axis(n) is a signed permutation (b.y = n; A = 0: b.x = -e_z,
+        // b.z = -fs e_y; A = 1, 2: b.x = -e_x, b.z = -fs e_z / fs e_y) and onb_transform(b, v) is
+        // exact: (fs v.y, -fs v.z, -v.x), (-v.x, fs v.y, -fs v.z), (-v.x, fs v.z, fs v.y) -- the same
+        // values without the cross products and the nine multiply-adds (signed zeros aside, which no
+        // later test can tell apart); dot(u, n) is fs u_A
+        auto cos_dir = [&](R u1, R u2) -> V<R> {
+          const V<R> v = cosine_dir(u1, u2);
+          if constexpr (FLAT) {
+            const R sy = fs * v.y, sz = fs * v.z;
+            return fA == 0 ? mkv(sy, -sz, -v.x) : (fA == 1 ? mkv(-v.x, sy, -sz) : mkv(-v.x, sz, sy));
+          } else {
+            return onb_transform(b, v);
+          }
+        };
+        auto cos_n = [&](V<R> u) -> R {  // dot(u, n) (onb.h's w = n)
+          if constexpr (FLAT) return fs * (fA == 0 ? u.x : (fA == 1 ? u.y : u.z));
+          return dot(u, b.y);
+        };
         const Light<R>* Lt = sc.light;  // read at the point of use (light_pdf, light_random)
         R pv;
         V<R> dir;
         if (ld_here(&Lt->kind) == L_NONE) {  // camera.h:217-226
           R u1 = U();
           R u2 = U();
-          dir = iso ? unit(on_sphere(u1, u2)) : onb_transform(b, cosine_dir(u1, u2));
-          pv = iso ? iso_pdf : fmax(R(0), div_pi(dot(unit(dir), b.y)));
+          dir = iso ? unit(on_sphere(u1, u2)) : cos_dir(u1, u2);
+          pv = iso ? iso_pdf : fmax(R(0), div_pi(cos_n(unit(dir))));
         } else {  // dual_pdf(hittable_pdf(light), material pdf) (camera.h:227-239, pdf.h:48-61)
           R c = U();
           R u1 = U();
@@ -692,15 +718,15 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
           if (from_light)
             dir = light_random(Lt, pw, u1, u2);
           else
-            dir = iso ? unit(on_sphere(u1, u2)) : onb_transform(b, cosine_dir(u1, u2));
-          R mp = iso ? iso_pdf : fmax(R(0), div_pi(dot(unit(dir), b.y)));
+            dir = iso ? unit(on_sphere(u1, u2)) : cos_dir(u1, u2);
+          R mp = iso ? iso_pdf : fmax(R(0), div_pi(cos_n(unit(dir))));
           pv = R(0.5) * light_pdf(Lt, pw, dir, from_light) + R(0.5) * mp;
         }
         R ps;
         if (iso) {
           ps = iso_pdf;
         } else {
-          R c = dot(n, unit(dir));
+          R c = FLAT ? cos_n(unit(dir)) : dot(n, unit(dir));
           ps = c < R(0) ? R(0) : div_pi(c);
         }
         if constexpr (sizeof(R) == 8)
