@@ -863,7 +863,7 @@ struct StackTrav {
 #define RT_WIDE_RELOAD 0
 #endif
 #ifndef RT_SHADE_BATCH  // < 64: a wave stops traversing to shade once this many of its lanes have finished
-#define RT_SHADE_BATCH 64  // (LDS-resident tree; measured on C3: 16 / 32 / 48 are 1-2 % slower than never pausing)
+#define RT_SHADE_BATCH 48  // (LDS-resident tree, C3 fp32 ms/frame: never 57.06, 48: 52.57, 52: 52.58, 56: 52.81, 60: 53.57; fp64 81.3 -> 75.8)
 #endif
 #ifndef RT_SHADE_BATCH_GLOBAL  // the same for trees in HBM (speculative traversal): C4 stand-in 413.6 ms/frame
 #define RT_SHADE_BATCH_GLOBAL 48  // never pausing, 415.2 / 370.8 / 363.8 / 362.5 / 368.4 / 379.6 at 16/32/40/48/56/60
