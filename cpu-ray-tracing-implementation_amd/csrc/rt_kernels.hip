@@ -587,8 +587,12 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
           // mirror / glass bounces to leave the fp64 path a few times per million segments),
           // then the point and normal (sphere.h:67-69) from the refined root. A step that does
           // not land near the fp32 root (a grazing double root) keeps it.
-          const double cx = (double)sp.c1[0] + (double)s.tm * sp.dc[0], cy = (double)sp.c1[1] + (double)s.tm * sp.dc[1],
-                       cz = (double)sp.c1[2] + (double)s.tm * sp.dc[2];
+          double cx = sp.c1[0], cy = sp.c1[1], cz = sp.c1[2];  // sphere.h:83 (a static sphere: dc = 0)
+          if (!unit_n) {
+            cx += (double)s.tm * sp.dc[0];
+            cy += (double)s.tm * sp.dc[1];
+            cz += (double)s.tm * sp.dc[2];
+          }
           // g(t0) = |o + t0 d - c|^2 - r^2 needs fp64 (it cancels); the step g / g' is tiny next
           // to t0, so g' = 2 d.(o + t0 d - c) and the quotient are fp32
           const double ox = oo.x, oy = oo.y, oz = oo.z, dx = dd.x, dy = dd.y, dz = dd.z, t0 = t, rr = sp.r;
