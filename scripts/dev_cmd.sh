@@ -1,10 +1,13 @@
 set -e
-mkdir -p gpurun_out/s14
-for c in "c2 f64" "c2 f32" "c3 f32" "c3 f64" "c4 f32" "c5 f32"; do
-  timeout -k 10 150 python3 scripts/dev_wide_stats.py $c >> gpurun_out/s14/stats.txt 2>&1
-done
-grep -v amdgpu.ids gpurun_out/s14/stats.txt
-timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/s14/smoke.log 2>&1
-tail -n 1 gpurun_out/s14/smoke.log
-timeout -k 10 300 python3 bench.py > gpurun_out/s14/bench_default.json 2> gpurun_out/s14/bench_default.err
-cut -c1-300 gpurun_out/s14/bench_default.json
+mkdir -p gpurun_out/s15
+B=cpu-ray-tracing-implementation_amd/build
+run() {  # tag lib config precision
+  L=""; [ $2 != base ] && L="RT_HIP_LIB=$B/librt_hip_$2.so"
+  env $L timeout -k 10 200 python3 bench.py --config $3 --precision $4 --steps 10 --no-cpu-baseline --alt-steps 0 > gpurun_out/s15/$1.json 2>gpurun_out/s15/$1.err
+  python3 -c "import json;d=json.load(open('gpurun_out/s15/$1.json'));print('$1',d['ms_per_step'], d['value'])"
+}
+run c2_f64_fw5 fw5 c2 f64
+run c2_f64_fw3 fw3 c2 f64
+run c2_f64_base base c2 f64
+run c4_f32_gw5 gw5 c4 f32
+run c4_f32_base base c4 f32
