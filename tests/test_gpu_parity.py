@@ -489,3 +489,31 @@ def test_auto_item_layout_with_tail_is_tiling_invariant(ctx, name, spp):
     np.testing.assert_allclose(uniform, base, rtol=1e-5, atol=1e-6)
     ref, _ = oracle.render(oracle.from_desc(desc), cam, spp, 8, seed=5)
     assert (rmse(base.astype(np.float64), ref) < 1e-3).all(), rmse(base.astype(np.float64), ref)
+
+
+def fog_without_light(moving):
+    """An isotropic medium and diffuse spheres under a sky, no light: every scatter draws from the material's
+    own pdf (isotropic, material.h:193-205; lambertian, material.h:62-80), whose ratio to p_scattered the device
+    does not evaluate (camera.h:217-226) -- plus, for fp64, a moving sphere, whose non-unit normal (sphere.h:69)
+    keeps the ratio (|n|: radiance grows along such paths, which makes fp32 against fp64 ill-conditioned)."""
+    s = SceneBuilder()
+    grey = s.lambertian(s.solid((0.6, 0.6, 0.6)))
+    blue = s.lambertian(s.solid((0.2, 0.3, 0.8)))
+    objs = [s.sphere((0, -100.5, -1), 100, grey), s.sphere((1.1, 0, -1.2), 0.5, blue),
+            s.moving_sphere((-1.1, 0, -1.2), (-1.1, 0.2, -1.2), 0.4, grey) if moving
+            else s.sphere((-1.1, 0, -1.2), 0.4, grey),
+            s.volume(s.sphere((0, 0.1, -1), 0.45, grey), 1.5, s.solid((0.9, 0.8, 0.7)))]
+    cam = perspective(48, 1.5, (0, 0.6, 1.5), (0, 0, -1), 1, 50.0)
+    return s.desc(s.hlist(objs), background=s.solid((0.7, 0.8, 1.0))), cam
+
+
+@pytest.mark.parametrize("precision", [F64, F32], ids=["f64", "f32"])
+def test_no_light_own_pdf_scatter_matches_oracle(ctx, precision):
+    desc, cam = fog_without_light(precision == F64)
+    img, ref, _ = render_both(ctx, desc, cam, 32, 10, 11, precision)
+    assert np.isfinite(img).all()
+    if precision == F64:
+        bad = (np.abs(img - ref) > 1e-9 * np.maximum(1.0, np.abs(ref))).any(-1)
+        assert bad.sum() <= 2, (int(bad.sum()), float(np.abs(img - ref).max()))
+    else:
+        assert (rmse(img, ref) < 1e-4).all(), rmse(img, ref)
