@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--pool", type=int, default=0)
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--ts", type=int, default=TILE, help="tile edge (default rt_amd.tiling.TILE)")
+    ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
     args = ap.parse_args()
     scene_name, width, aspect, spp, depth = CONFIGS[args.config]
     cs = plugin.ConfigScene(scene_name, width, aspect)
@@ -39,11 +40,12 @@ def main():
     dev = torch.device("cuda", 0)
     ctx = rt_amd.Context(0)
     ctx.upload(cs.desc)
-    params = ctx.params(spp, depth, 1, abi.RT_PREC_F32, samples_per_item=args.chunk, pool_slots=args.pool)
+    prec = abi.RT_PREC_F64 if args.precision == "f64" else abi.RT_PREC_F32
+    params = ctx.params(spp, depth, 1, prec, samples_per_item=args.chunk, pool_slots=args.pool)
     base = None
     for world in [int(x) for x in args.worlds.split(",")]:
         all_tiles, counts, maxpix = plan(W, H, world, ts=args.ts)
-        out = torch.zeros((maxpix, 3), dtype=torch.float32, device=dev)
+        out = torch.zeros((maxpix, 3), dtype=torch.float64 if args.precision == "f64" else torch.float32, device=dev)
         per_rank, kern = [], []
         for r in range(world):
             stream = torch.cuda.current_stream(dev).cuda_stream
