@@ -321,8 +321,6 @@ struct DevScene {
   uint32_t n_wnodes, n_wprim_words, wroot, wide_stack, wide_kinds;
   int32_t has_wide;
   uint32_t wide_big;  // primitives at the head of the word stream, tested before the tree
-  const void* wnodesq;  // the quantised tree over the same leaves (WNodeQ4 / WNode8 by wideq_width; 0: none)
-  uint32_t wrootq, wideq_stack, wideq_width;
   // a tree in HBM keeps at most kWideLdsStack stack entries per lane in LDS; deeper entries (rare:
   // every child of every node on a path hit) go to wide_spill[(depth - kWideLdsStack) * spill_lanes + lane]
   uint32_t* wide_spill;
@@ -641,14 +639,16 @@ __device__ __forceinline__ R comp(V<R> v) {
 // order of the bit patterns, so with 0 < tmin <= tmax
 //   tmin <= t <= tmax        <=>  bits(t) - bits(tmin) <= bits(tmax) - bits(tmin)  (unsigned)
 //   0 <= alpha, beta <= 1     <=>  max(bits(alpha), bits(beta)) <= bits(1.0f)
-// and NaN or negative values fail both (only alpha = -0.0, an exact edge hit, is decided
-// differently). One compare each instead of a branch per condition.
+// and NaN or negative values fail both. One compare each instead of a branch per condition.
+// alpha = (p - lo) * inv is -0.0 on the quad's Q edge when inv < 0 (a negative edge vector, as
+// box() faces have), which the reference accepts (0 <= -0.0) and the bit order would not: the
+// product is formed as fma(p - lo, inv, +0.0), equal to it except that -0.0 becomes +0.0.
 template <int A, int U, int W, class R>
 __device__ __forceinline__ bool aquad_t(const R* f, V<R> o, V<R> d, V<R> inv, R tmin, R tmax, R& t) {
   R th = fdiv_inv(f[0] - comp<A>(o), comp<A>(d), comp<A>(inv));
   if constexpr (sizeof(R) == 4) {
-    const R a = ((comp<U>(o) + th * comp<U>(d)) - f[1]) * f[3];
-    const R b = ((comp<W>(o) + th * comp<W>(d)) - f[2]) * f[4];
+    const R a = __builtin_fmaf((comp<U>(o) + th * comp<U>(d)) - f[1], f[3], 0.0f);
+    const R b = __builtin_fmaf((comp<W>(o) + th * comp<W>(d)) - f[2], f[4], 0.0f);
     const uint32_t lo = __float_as_uint(tmin);
     const bool in_t = __float_as_uint(th) - lo <= __float_as_uint(tmax) - lo;
     const bool in_ab = max(__float_as_uint(a), __float_as_uint(b)) <= 0x3f800000u;
@@ -976,94 +976,18 @@ __host__ __device__ __forceinline__ uint32_t wide_code16(uint32_t c) {
 }
 template <bool LDSN>
 using WStackT = typename std::conditional<LDSN, uint16_t, uint32_t>::type;
-// slab distances of the 8 children of a compressed node (rt_scene.h WNode8) as sort keys
-// (bits(t_near) with the slot in the low 3 bits; 0xFFFFFFFF: missed or unused). A plane's distance
-// is fma(q, s * inv, (o_node - o) * inv): the quantum and origin are folded into the ray once per
-// node, so a child plane costs one byte conversion (v_cvt_f32_ubyte) and one fma.
-__device__ __forceinline__ void wide8_keys(const WNode8* node, V<float> o, V<float> inv, float tmin, float tmax,
-                                           uint32_t k[8], uint4& c0, uint4& c1) {
-  const uint4* nd = (const uint4*)node;
-  const uint4 h = nd[0], qa = nd[1], qb = nd[2], qc = nd[3];
-  c0 = nd[4];
-  c1 = nd[5];
-  const float ax = __uint_as_float((h.w & 0xFFu) << 23) * inv.x, bx = (__uint_as_float(h.x) - o.x) * inv.x;
-  const float ay = __uint_as_float(((h.w >> 8) & 0xFFu) << 23) * inv.y, by = (__uint_as_float(h.y) - o.y) * inv.y;
-  const float az = __uint_as_float(((h.w >> 16) & 0xFFu) << 23) * inv.z, bz = (__uint_as_float(h.z) - o.z) * inv.z;
-  const uint32_t n = h.w >> 24;
-  // qlo x: qa.x (slots 0-3), qa.y (4-7); y: qa.z, qa.w; z: qb.x, qb.y. qhi x: qb.z, qb.w; y: qc.x, qc.y; z: qc.z, qc.w
-#pragma unroll
-  for (int c = 0; c < 8; c++) {
-    const int sh = 8 * (c & 3);
-    const bool hi4 = c >= 4;
-    auto q = [&](uint32_t w) { return (float)((w >> sh) & 0xFFu); };
-    const float tx0 = fmaf(q(hi4 ? qa.y : qa.x), ax, bx), tx1 = fmaf(q(hi4 ? qb.w : qb.z), ax, bx);
-    const float ty0 = fmaf(q(hi4 ? qa.w : qa.z), ay, by), ty1 = fmaf(q(hi4 ? qc.y : qc.x), ay, by);
-    const float tz0 = fmaf(q(hi4 ? qb.y : qb.x), az, bz), tz1 = fmaf(q(hi4 ? qc.w : qc.z), az, bz);
-    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
-    const float tf =
-        fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax)) * Num<float>::box_slack();
-    k[c] = ((uint32_t)c < n && tn <= tf) ? ((__float_as_uint(tn) & ~7u) | (uint32_t)c) : 0xFFFFFFFFu;
-  }
-  // sort near to far: the 19-comparator network for 8 inputs
-#define RT_CS8(a, b)                          \
-  {                                           \
-    const uint32_t lo_ = min(k[a], k[b]);     \
-    k[b] = max(k[a], k[b]);                   \
-    k[a] = lo_;                               \
-  }
-  RT_CS8(0, 2) RT_CS8(1, 3) RT_CS8(4, 6) RT_CS8(5, 7)
-  RT_CS8(0, 4) RT_CS8(1, 5) RT_CS8(2, 6) RT_CS8(3, 7)
-  RT_CS8(0, 1) RT_CS8(2, 3) RT_CS8(4, 5) RT_CS8(6, 7)
-  RT_CS8(2, 4) RT_CS8(3, 5)
-  RT_CS8(1, 4) RT_CS8(3, 6)
-  RT_CS8(1, 2) RT_CS8(3, 4) RT_CS8(5, 6)
-#undef RT_CS8
-}
-// the same for the four children of a quantised 4-wide node (rt_scene.h WNodeQ4), sorted by the
-// 5-comparator network of the float nodes
-__device__ __forceinline__ void wideq4_keys(const WNodeQ4* node, V<float> o, V<float> inv, float tmin, float tmax,
-                                            uint32_t& k0, uint32_t& k1, uint32_t& k2, uint32_t& k3, uint4& cc) {
-  const uint4* nd = (const uint4*)node;
-  const uint4 h = nd[0], qa = nd[1], qb = nd[2];  // qa: qlo x, y, z, qhi x; qb: qhi y, z
-  cc = nd[3];
-  const float ax = __uint_as_float((h.w & 0xFFu) << 23) * inv.x, bx = (__uint_as_float(h.x) - o.x) * inv.x;
-  const float ay = __uint_as_float(((h.w >> 8) & 0xFFu) << 23) * inv.y, by = (__uint_as_float(h.y) - o.y) * inv.y;
-  const float az = __uint_as_float(((h.w >> 16) & 0xFFu) << 23) * inv.z, bz = (__uint_as_float(h.z) - o.z) * inv.z;
-  const uint32_t n = h.w >> 24;
-  uint32_t k[4];
-#pragma unroll
-  for (int c = 0; c < 4; c++) {
-    const int sh = 8 * c;
-    auto q = [&](uint32_t w) { return (float)((w >> sh) & 0xFFu); };
-    const float tx0 = fmaf(q(qa.x), ax, bx), tx1 = fmaf(q(qa.w), ax, bx);
-    const float ty0 = fmaf(q(qa.y), ay, by), ty1 = fmaf(q(qb.x), ay, by);
-    const float tz0 = fmaf(q(qa.z), az, bz), tz1 = fmaf(q(qb.y), az, bz);
-    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
-    const float tf =
-        fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax)) * Num<float>::box_slack();
-    k[c] = ((uint32_t)c < n && tn <= tf) ? ((__float_as_uint(tn) & ~3u) | (uint32_t)c) : 0xFFFFFFFFu;
-  }
-  k0 = k[0], k1 = k[1], k2 = k[2], k3 = k[3];
-}
-// the child code in slot (key & 7) of the node whose codes are c0 (slots 0-3) and c1 (4-7)
-__device__ __forceinline__ uint32_t wide8_child(uint32_t key, const uint4& c0, const uint4& c1) {
-  const uint4 c = (key & 4u) ? c1 : c0;
-  const uint32_t lo = (key & 1u) ? c.y : c.x, hi = (key & 1u) ? c.w : c.z;
-  return (key & 2u) ? hi : lo;
-}
 // fp64 rays (round 3) traverse the same float boxes: the ray is rounded to float for the slab tests
 // and every slab is widened by the distance the rounding moved the origin along that axis, |delta_a|
 // / |d_a| (delta = o - float(o), exact in double, scaled by 1 + 2^-20), the direction's rounding
 // being covered, like the fp32 path's own, by the relative box_slack of the exit distance; the
 // lower bound is 0.00099 instead of 0.001. The boxes only cull: the primitive tests are the fp64
 // ones of the other fp64 traversals, so the closest hit is theirs (exact-t ties aside).
-template <class R, bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN, int BLOCK, int PAUSE, int QN = 0>
+template <class R, bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN, int BLOCK, int PAUSE>
 __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned char* lds_nodes,
                                            const typename WWord<R>::T* lds_prims, V<R> ro, V<R> rd, R time,
                                            uint32_t excl_e, WStackT<LDSN>* stk, WideRayT<R>& ry) {
   using WW = typename WWord<R>::T;
   constexpr bool F64 = sizeof(R) == 8;
-  static_assert(QN == 0 || (!LDSN && RT_WIDE_SPEC && !F64), "quantised nodes: fp32, traversed speculatively, from HBM");
   constexpr uint32_t kLeafBit = LDSN ? kWLeaf16 : kWLeaf;
   const R tmin = R(0.001);
   const float tmin_box = F64 ? 0.00099f : 0.001f;
@@ -1256,32 +1180,12 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
           break;
         }
         cur = pop();
-      } else if constexpr (QN == 8) {  // a compressed 8-wide node (HBM trees)
-        uint32_t k[8];
-        uint4 c0, c1;
-        wide8_keys((const WNode8*)sc.wnodesq + cur, o, inv, tmin, tmax, k, c0, c1);
-        if (k[0] == 0xFFFFFFFFu) {
-          if (sp == 0) {
-            have = false;
-            break;
-          }
-          cur = pop();
-        } else {
-#pragma unroll
-          for (int j = 7; j >= 1; j--)
-            if (k[j] != 0xFFFFFFFFu) push(wide8_child(k[j], c0, c1));
-          cur = wide8_child(k[0], c0, c1);
-        }
       } else {
         const OfsT nof = node_off(cur);
         uint4 cc{};
         uint32_t k0, k1, k2, k3;
-        if constexpr (QN == 4) {  // a quantised 4-wide node (HBM trees)
-          wideq4_keys((const WNodeQ4*)sc.wnodesq + cur, o, inv, tmin, tmax, k0, k1, k2, k3, cc);
-        } else {
-          if constexpr (!LDSN) cc = *(const uint4*)(nbase + (nof + 96u));
-          node_keys(nof, k0, k1, k2, k3);
-        }
+        if constexpr (!LDSN) cc = *(const uint4*)(nbase + (nof + 96u));
+        node_keys(nof, k0, k1, k2, k3);
         auto child = [&](uint32_t k) -> uint32_t {
           if constexpr (LDSN) {
             return ((const uint16_t*)(nbase + (nof + 96u)))[k & 3u];
@@ -1496,8 +1400,9 @@ __device__ __forceinline__ void flat_quad_test(const FlatQuadT<R>& r, int32_t id
                                                R tmin, R& tmax, int32_t& best, uint64_t xkey) {
   constexpr int U = A == 0 ? 1 : 0, W = A == 2 ? 1 : 2;
   const R th = (r.plane - comp<A>(o)) * comp<A>(inv);
-  const R a = ((comp<U>(o) + th * comp<U>(d)) - r.lo_u) * r.inv_u;
-  const R b = ((comp<W>(o) + th * comp<W>(d)) - r.lo_w) * r.inv_w;
+  // fma(., inv, +0.0): the product, with an exact edge hit's -0.0 as +0.0 (aquad_t)
+  const R a = fma((comp<U>(o) + th * comp<U>(d)) - r.lo_u, r.inv_u, R(0));
+  const R b = fma((comp<W>(o) + th * comp<W>(d)) - r.lo_w, r.inv_w, R(0));
   bool in_t, in_ab;
   if constexpr (sizeof(R) == 4) {
     const uint32_t lo = __float_as_uint(tmin);

@@ -892,7 +892,7 @@ struct StackTrav {
 #ifndef RT_WIDE_WAVES_GLOBAL_F64  // tree in HBM (C4 fp64: 3 waves 599.8, 4: 555.0, 5: 567.3)
 #define RT_WIDE_WAVES_GLOBAL_F64 4
 #endif
-template <class R, bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN, int QN = 0>
+template <class R, bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN>
 struct WideTrav {
   static constexpr int kStack = 0;
   static constexpr int kLdsNodes = 0;
@@ -908,7 +908,7 @@ struct WideTrav {
     return LDSN ? n_wnodes * kWNodeLdsStride + n_words * (uint32_t)sizeof(WW) : 0u;
   }
   __host__ __device__ static uint32_t root(const DevScene<R>& sc) {
-    return QN ? sc.wrootq : (LDSN ? wide_code16(sc.wroot) : sc.wroot);
+    return LDSN ? wide_code16(sc.wroot) : sc.wroot;
   }
   __device__ __forceinline__ static StackT* fill(const DevScene<R>& sc, uint4* lds) {
     unsigned char* base = (unsigned char*)lds;
@@ -934,7 +934,7 @@ struct WideTrav {
   __device__ __forceinline__ static bool steps(const DevScene<R>& sc, const Node<R>* lds, const PS& s, StackT* stk,
                                                WideRayT<R>& ry) {
     const unsigned char* base = (const unsigned char*)lds;
-    return trace_wide<R, SPH, TRI, QUAD, MOV, LDSN, kBlock, LDSN ? RT_SHADE_BATCH : RT_SHADE_BATCH_GLOBAL, QN>(
+    return trace_wide<R, SPH, TRI, QUAD, MOV, LDSN, kBlock, LDSN ? RT_SHADE_BATCH : RT_SHADE_BATCH_GLOBAL>(
         sc, base, (const WW*)(base + sc.n_wnodes * kWNodeLdsStride), s.o, s.d, s.tm, s.xe, stk, ry);
   }
 };
@@ -1495,10 +1495,6 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
   s.wide_stack = h.wide_stack;
   s.wide_kinds = h.wide_kinds;
   s.wide_big = h.wide_big;
-  s.wnodesq = at(h.off_wnodesq);
-  s.wrootq = h.wrootq;
-  s.wideq_stack = h.wideq_stack;
-  s.wideq_width = h.wideq_width;
   return s;
 }
 
@@ -1543,10 +1539,10 @@ void launch_one(KernelT kern, Params<R> p, uint32_t grid, hipStream_t st, size_t
 // Dynamic LDS of a wide-BVH launch: the whole tree when it fits the budget (LDSN), else the stack only.
 constexpr size_t kWideLdsBudget = 40u << 10;  // bytes per 256-lane block: 4 blocks per CU of 160 KiB
 template <class R>
-inline size_t wide_lds_bytes(const DevScene<R>& sc, bool ldsn, bool w8 = false) {
+inline size_t wide_lds_bytes(const DevScene<R>& sc, bool ldsn) {
   // an LDS tree: every entry in LDS, uint16; a tree in HBM: up to kWideLdsStack uint32 entries (the rest spill)
   const size_t stack = ldsn ? (size_t)sc.wide_stack * kBlock * 2u
-                            : (size_t)std::min<uint32_t>(w8 ? sc.wideq_stack : sc.wide_stack, kWideLdsStack) * kBlock * 4u;
+                            : (size_t)std::min<uint32_t>(sc.wide_stack, kWideLdsStack) * kBlock * 4u;
   return (ldsn ? (size_t)sc.n_wnodes * kWNodeLdsStride + (size_t)sc.n_wprim_words * sizeof(typename WWord<R>::T) : 0u) +
          stack;
 }
@@ -1558,18 +1554,6 @@ void launch_wide_k(const Params<R>& p, uint32_t grid, hipStream_t st) {
   if (full <= kWideLdsBudget && p.sc.n_wnodes * kWNodeLdsUnits < 0x8000u && p.sc.n_wprim_words <= 0x1000u) {
     launch_one(k_persist_occ<R, WideTrav<R, SPH, TRI, QUAD, MOV, true>, false>, p, grid, st, full);
     return;
-  }
-  if constexpr (sizeof(R) == 4) {  // the quantised trees (fp32; opt-in, RT_DEV_WIDEQ)
-    if (p.sc.wideq_width == 4) {
-      launch_one(k_persist_occ<R, WideTrav<R, SPH, TRI, QUAD, MOV, false, 4>, false>, p, spill_grid, st,
-                 wide_lds_bytes(p.sc, false, true));
-      return;
-    }
-    if (p.sc.wideq_width == 8) {
-      launch_one(k_persist_occ<R, WideTrav<R, SPH, TRI, QUAD, MOV, false, 8>, false>, p, spill_grid, st,
-                 wide_lds_bytes(p.sc, false, true));
-      return;
-    }
   }
   // the spill area holds spill_lanes lanes: never launch more (the resident grid is below it)
   launch_one(k_persist_occ<R, WideTrav<R, SPH, TRI, QUAD, MOV, false>, false>, p, spill_grid, st,
@@ -1762,7 +1746,7 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     unsigned char* sp = (unsigned char*)c->state.ptr;
     Params<R> p{};
     p.sc = dev_scene<R>(hdr, sbase);
-    const uint32_t wide_need = std::max(hdr.wide_stack, hdr.wideq_width ? hdr.wideq_stack : 0u);
+    const uint32_t wide_need = hdr.wide_stack;
     if (hdr.has_wide && wide_need > kWideLdsStack) {
       // a deep wide tree: a spill area of (need - kWideLdsStack) entries for every lane the chip can hold
       int ncu = 0;
@@ -2081,12 +2065,14 @@ rt_status rt_set_timing(rt_context* c, int32_t enable) {
 
 #ifdef RT_SECTION_CLOCKS
 // development build only (scripts/dev_sections.py): read and clear the section clocks
-void rt_dev_section_clocks(unsigned long long out[7]) {
-  hipMemcpyFromSymbol(out, HIP_SYMBOL(g_section_clocks), sizeof(unsigned long long) * 4);
-  hipMemcpyFromSymbol(out + 4, HIP_SYMBOL(rtd::g_trace_totals), sizeof(unsigned long long) * 3);
-  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  hipMemcpyToSymbol(HIP_SYMBOL(g_section_clocks), z, sizeof(z));
-  hipMemcpyToSymbol(HIP_SYMBOL(rtd::g_trace_totals), z, sizeof(unsigned long long) * 3);
+int rt_dev_section_clocks(unsigned long long out[7]) {
+  const unsigned long long z[4] = {0, 0, 0, 0};
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_section_clocks), sizeof(unsigned long long) * 4);
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(out + 4, HIP_SYMBOL(rtd::g_trace_totals), sizeof(unsigned long long) * 3);
+  // each symbol is cleared with its own size (g_section_clocks: 4 entries, g_trace_totals: 3)
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_section_clocks), z, sizeof(unsigned long long) * 4);
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(rtd::g_trace_totals), z, sizeof(unsigned long long) * 3);
+  return e == hipSuccess ? 0 : -1;
 }
 // the wide kernels' wave-level counts (rt_device.h g_wide_stats), read and cleared
 void rt_dev_wide_stats(unsigned long long out[10]) {

@@ -206,36 +206,6 @@ struct alignas(16) WNode {
   uint32_t child[4];
   uint32_t pad[4];
 };
-// The compressed 8-wide node (round 3; opt-in, RT_DEV_WIDEQ=8) for trees that stay in HBM: child boxes
-// quantised to 8 bits per plane against the node's origin with a power-of-two quantum per axis
-// (Ylitie, Karras & Laine 2017), so one node holds 8 children in 96 B where the 4-wide node needs
-// 128 B for 4, and a ray's path from the root has half the levels -- half the dependent fetches.
-//   child k's box on axis a: [o_a + qlo_a[k] s_a, o_a + qhi_a[k] s_a], s_a = 2^(e_a - 127);
-//   the builder rounds outward and pads one quantum on each side, so the box is conservative.
-//   qlo / qhi: for axis a, words 2a and 2a + 1 hold the bytes of slots 0-3 and 4-7.
-//   meta: bytes 0-2 e_x, e_y, e_z; byte 3 the children in use (slots 0..n-1).
-//   child[k]: as WNode (an inner node's index in the 8-wide array, or a leaf code).
-struct alignas(16) WNode8 {
-  float ox, oy, oz;
-  uint32_t meta;
-  uint32_t qlo[6];
-  uint32_t qhi[6];
-  uint32_t child[8];
-};
-static_assert(sizeof(WNode8) == 96, "WNode8 is six 16-byte loads");
-// The quantised 4-wide node (round 3; opt-in, RT_DEV_WIDEQ=4): WNode's four children with WNode8's
-// quantised boxes in 64 B instead of 128 -- the C4 stand-in's 42,902 nodes fit in 2.7 MB, under one
-// XCD's 4 MB L2 -- measured slower than the float node there (scene_compile.cpp wide_bvh).
-// qlo[a] / qhi[a]: byte c = child c's plane on axis a.
-struct alignas(16) WNodeQ4 {
-  float ox, oy, oz;
-  uint32_t meta;
-  uint32_t qlo[3];
-  uint32_t qhi[3];
-  uint32_t pad[2];
-  uint32_t child[4];
-};
-static_assert(sizeof(WNodeQ4) == 64, "WNodeQ4 is four 16-byte loads");
 constexpr uint32_t kWLeaf = 0x80000000u;
 constexpr uint32_t kWCountShift = 25;  // leaf: up to 64 primitives, first word < 2^25
 constexpr uint32_t kWFirstMask = (1u << kWCountShift) - 1u;
@@ -318,12 +288,6 @@ struct SceneHeader {
   uint32_t wide_kinds;   // WK_* bits
   uint32_t has_wide;
   uint32_t wide_big;     // primitives at the head of the word stream tested before the tree (huge boxes)
-  uint32_t wrootq;       // the quantised tree over the same leaves (wideq_width 4 or 8; 0: none): root code
-  uint32_t wideq_stack;  // its stack need
-  uint32_t wideq_width;
-  uint64_t off_wnodesq;
-  uint32_t n_wnodesq;
-  uint32_t wideq_pad_;
 };
 
 }  // namespace rtd

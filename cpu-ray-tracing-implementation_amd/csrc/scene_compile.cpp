@@ -1263,82 +1263,6 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
                  words.size(), bn.size());
   if (!ok || need > kWideStackMax) return false;
 
-  // The compressed 8-wide tree (rt_scene.h WNode8) over the same leaves, for the kernels that keep
-  // the tree in HBM. Quantisation per node: origin = the node box's low corner rounded down to
-  // float, quantum s_a = the power of two with (hi_a - o_a) / s_a <= 253, child planes rounded
-  // outward (the kernel's rounding of plane distances is covered by the slab test's relative
-  // widening, box_slack, as for the float boxes of the 4-wide nodes).
-  // A quantised tree over the same leaves (rt_scene.h WNodeQ4 / WNode8), for the kernels that keep
-  // the tree in HBM. Quantisation per node: origin = the node box's low corner rounded down to
-  // float, quantum s_a = the power of two with (hi_a - o_a) / s_a <= 253, child planes rounded
-  // outward (the kernel's rounding of plane distances is covered by the slab test's relative
-  // widening, box_slack, as for the float boxes of the 4-wide nodes).
-  struct QN {
-    float o[3];
-    uint32_t meta;
-    uint32_t qlo[3][8], qhi[3][8];
-    uint32_t child[8];
-  };
-  std::vector<QN> qn;
-  const char* wq_env = std::getenv("RT_DEV_WIDEQ");
-  const int qwidth = wq_env ? std::atoi(wq_env) : 0;
-  std::function<bool(int, uint32_t&, int&)> emitq = [&](int b, uint32_t& code, int& needq) -> bool {
-    const BN& nd = bn[(size_t)b];
-    if (nd.left < 0) {
-      needq = 0;
-      return leaf_code(b, code);
-    }
-    const std::vector<int> ch = collapse(b, (size_t)qwidth);
-    const size_t idx = qn.size();
-    if (idx >= kWLeaf) return false;
-    qn.emplace_back();
-    Box nb;
-    for (int c : ch) nb.grow(bn[(size_t)c].box);
-    QN w{};
-    double sc[3];
-    int ex[3];
-    for (int a = 0; a < 3; a++) {
-      w.o[a] = down(nb.lo[a]);
-      const double ext = nb.hi[a] - (double)w.o[a];
-      int e = -100;
-      if (ext > 0) e = std::max(-126, (int)std::ceil(std::log2(ext / 253.0)));
-      while (std::ldexp(253.0, e) < ext) e++;
-      if (e > 127) return false;
-      ex[a] = e;
-      sc[a] = std::ldexp(1.0, e);
-    }
-    w.meta = (uint32_t)(ex[0] + 127) | (uint32_t)(ex[1] + 127) << 8 | (uint32_t)(ex[2] + 127) << 16 |
-             (uint32_t)ch.size() << 24;
-    for (size_t c = 0; c < ch.size(); c++) {
-      const Box& bx = bn[(size_t)ch[c]].box;
-      for (int a = 0; a < 3; a++) {
-        const double lo = std::floor((bx.lo[a] - (double)w.o[a]) / sc[a]);
-        const double hi = std::ceil((bx.hi[a] - (double)w.o[a]) / sc[a]);
-        w.qlo[a][c] = (uint32_t)std::min(255.0, std::max(0.0, lo));
-        w.qhi[a][c] = (uint32_t)std::min(255.0, std::max(0.0, hi));
-      }
-    }
-    int sub = 0;
-    for (size_t c = 0; c < ch.size(); c++) {
-      uint32_t cc;
-      int cn;
-      if (!emitq(ch[c], cc, cn)) return false;
-      sub = std::max(sub, cn);
-      w.child[c] = cc;
-    }
-    qn[idx] = w;
-    needq = (int)ch.size() - 1 + sub;
-    code = (uint32_t)idx;
-    return true;
-  };
-  uint32_t rootq = 0;
-  int needq = 0;
-  // RT_DEV_WIDEQ (development A/B; default 0: none, the float 4-wide tree serves HBM too): 4 the
-  // quantised 4-wide tree, 8 the compressed 8-wide one. Both measured slower on the C4 stand-in
-  // (r03j, ms/frame: float 4-wide 362.7, quantised 4-wide 386.5, 8-wide 506.0): the kernel there is
-  // bound by VALU issue in traversal, and dequantising the planes (and for 8-wide, a 19-comparator
-  // sort per visit) costs more than the smaller nodes and the halved fetch depth save.
-  const bool okq = (qwidth == 4 || qwidth == 8) && emitq(0, rootq, needq) && needq <= kWideStackMax;
   // two zero words past the last record: kernels with triangles read a record's next two words with
   // its first (trace_wide test_prims), past the end for a trailing sphere
   words.push_back({0.f, 0.f, 0.f, 0.f});
@@ -1371,41 +1295,6 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
   h.wide_kinds = kinds;
   h.wide_big = (uint32_t)big.size();
   h.has_wide = 1;
-  if (okq) {
-    if (qwidth == 8) {
-      std::vector<WNode8> v(qn.size());
-      for (size_t i = 0; i < qn.size(); i++) {
-        WNode8& w = v[i];
-        w.ox = qn[i].o[0], w.oy = qn[i].o[1], w.oz = qn[i].o[2], w.meta = qn[i].meta;
-        for (int a = 0; a < 3; a++)
-          for (int c = 0; c < 8; c++) {
-            w.qlo[2 * a + c / 4] |= qn[i].qlo[a][c] << (8 * (c % 4));
-            w.qhi[2 * a + c / 4] |= qn[i].qhi[a][c] << (8 * (c % 4));
-          }
-        for (int c = 0; c < 8; c++) w.child[c] = qn[i].child[c];
-      }
-      h.off_wnodesq = append(out->blob32, v);
-    } else {
-      std::vector<WNodeQ4> v(qn.size());
-      for (size_t i = 0; i < qn.size(); i++) {
-        WNodeQ4& w = v[i];
-        w.ox = qn[i].o[0], w.oy = qn[i].o[1], w.oz = qn[i].o[2], w.meta = qn[i].meta;
-        for (int a = 0; a < 3; a++)
-          for (int c = 0; c < 4; c++) {
-            w.qlo[a] |= qn[i].qlo[a][c] << (8 * c);
-            w.qhi[a] |= qn[i].qhi[a][c] << (8 * c);
-          }
-        for (int c = 0; c < 4; c++) w.child[c] = qn[i].child[c];
-      }
-      h.off_wnodesq = append(out->blob32, v);
-    }
-    out->blob32.resize((out->blob32.size() + 255) & ~size_t(255));
-    h.bytes = out->blob32.size();
-    h.n_wnodesq = (uint32_t)qn.size();
-    h.wrootq = rootq;
-    h.wideq_stack = (uint32_t)std::max(1, needq);
-    h.wideq_width = (uint32_t)qwidth;
-  }
   return true;
 }
 

@@ -117,35 +117,35 @@ class camera {
       out = px32.data();
     }
     if (!devices_.empty()) {  // the image tiled over several GPUs, one RCCL gather (rt_multi_*)
-      if (!multi_ || multi_devs_ != devices_) {  // kept across renders on the same devices
-        multi_.reset();
+      if (!h_.multi || h_.multi_devs != devices_) {  // kept across renders on the same devices
+        h_.multi.reset();
         rt_multi* mg = nullptr;
         if (rt_multi_create(devices_.data(), (int32_t)devices_.size(), &mg) != RT_OK)
           return fail(rt_multi_last_error(nullptr));
-        multi_.reset(mg, rt_multi_destroy);
-        multi_devs_ = devices_;
+        h_.multi.reset(mg, rt_multi_destroy);
+        h_.multi_devs = devices_;
       }
-      rt_status s = rt_multi_scene_upload(multi_.get(), &desc);
-      if (s == RT_OK) s = rt_multi_render(multi_.get(), &cam, &p, tile_size_, out);
+      rt_status s = rt_multi_scene_upload(h_.multi.get(), &desc);
+      if (s == RT_OK) s = rt_multi_render(h_.multi.get(), &cam, &p, tile_size_, out);
       if (s != RT_OK) {
-        std::string m = rt_multi_last_error(multi_.get());
-        multi_.reset();
+        std::string m = rt_multi_last_error(h_.multi.get());
+        h_.multi.reset();
         return fail(m);
       }
     } else {
-      if (!ctx_ || ctx_dev_ != device_) {  // kept across renders on the same device
-        ctx_.reset();
+      if (!h_.ctx || h_.ctx_dev != device_) {  // kept across renders on the same device
+        h_.ctx.reset();
         rt_context* c = nullptr;
         if (rt_context_create(device_, &c) != RT_OK) return fail(rt_last_error(nullptr));
-        ctx_.reset(c, rt_context_destroy);
-        ctx_dev_ = device_;
+        h_.ctx.reset(c, rt_context_destroy);
+        h_.ctx_dev = device_;
       }
       rt_tile tile{0, 0, image_width_, image_height_};
-      rt_status s = rt_scene_upload(ctx_.get(), &desc);
-      if (s == RT_OK) s = rt_render_tiles(ctx_.get(), &cam, &p, &tile, 1, out, 0, nullptr);
+      rt_status s = rt_scene_upload(h_.ctx.get(), &desc);
+      if (s == RT_OK) s = rt_render_tiles(h_.ctx.get(), &cam, &p, &tile, 1, out, 0, nullptr);
       if (s != RT_OK) {
-        std::string m = rt_last_error(ctx_.get());
-        ctx_.reset();
+        std::string m = rt_last_error(h_.ctx.get());
+        h_.ctx.reset();
         return fail(m);
       }
     }
@@ -238,8 +238,18 @@ class camera {
   }
   // The device handles of the last render, reused while devices_ / device_ stay the same: a context
   // per device and, for devices_, one RCCL communicator -- created once, not once per render().
-  std::shared_ptr<rt_multi> multi_;
-  std::vector<int32_t> multi_devs_;
-  std::shared_ptr<rt_context> ctx_;
-  int ctx_dev_ = -1;
+  // They belong to this camera: a copy starts without them (and copy assignment keeps the target's
+  // own), so two cameras never share a context's buffers and stream, and copies may render from
+  // different threads as before. One camera must still not render from two threads at once.
+  struct handles {
+    std::shared_ptr<rt_multi> multi;
+    std::vector<int32_t> multi_devs;
+    std::shared_ptr<rt_context> ctx;
+    int ctx_dev = -1;
+    handles() = default;
+    handles(const handles&) {}
+    handles& operator=(const handles&) { return *this; }
+    handles(handles&&) = default;
+    handles& operator=(handles&&) = default;
+  } h_;
 };

@@ -4,7 +4,8 @@ import sys
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for p in (os.path.join(REPO, "cpu-ray-tracing-implementation_amd", "python"), os.path.join(REPO, "oracle"), REPO):
+for p in (os.path.join(REPO, "cpu-ray-tracing-implementation_amd", "python"), os.path.join(REPO, "oracle"), REPO,
+          os.path.join(REPO, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)
 
@@ -12,6 +13,13 @@ for p in (os.path.join(REPO, "cpu-ray-tracing-implementation_amd", "python"), os
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")
     config.addinivalue_line("markers", "slow: CPU test taking more than a few seconds")
+    # The multi-process GPU test (test_gpu_multiprocess.py) starts its ranks from a forkserver, which
+    # must exist before this process touches the GPU: its children are forked from a process that
+    # never initialised HIP, and nothing is exec'ed from one that did.
+    expr = config.getoption("markexpr", default="") or ""
+    if "gpu" in expr and "not gpu" not in expr:
+        import multiprocessing.forkserver
+        multiprocessing.forkserver.ensure_running()
 
 
 @pytest.fixture(scope="session")

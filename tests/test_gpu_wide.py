@@ -139,21 +139,6 @@ def test_pixel_map_follows_the_last_tiles_height(ctx):
     assert np.array_equal(again.reshape(fresh.shape), fresh)
 
 
-@pytest.mark.parametrize("wq", ["4", "8"])
-def test_other_hbm_trees_match_binary(ctx, tmp_path, monkeypatch, wq):
-    # the tree in HBM is the float 4-wide one by default; RT_DEV_WIDEQ at scene compile selects the
-    # quantised 4-wide nodes (4, rt_scene.h WNodeQ4) or the compressed 8-wide ones (8, WNode8). Quantised
-    # child boxes must stay conservative: the closest hits equal the binary BVH's (ties aside)
-    from rt_amd import synth_gltf
-    monkeypatch.setenv("RT_SPONZA_GLTF", synth_gltf.write_sponza_standin(str(tmp_path)))
-    monkeypatch.setenv("RT_DEV_WIDEQ", wq)
-    cs = plugin.ConfigScene("sponza", 64, 16.0 / 9.0)
-    wide, binary = both_traversals(ctx, cs.desc, cs.cam, 4, 5, 3)
-    differ = np.abs(wide - binary).max(-1) > 0
-    assert differ.mean() < 5e-3, int(differ.sum())
-    assert (rmse(wide, binary) < 1e-4).all(), rmse(wide, binary)
-
-
 def both_traversals_f64(ctx, desc, cam, spp, depth, seed):
     ctx.upload(desc)
     wide = ctx.render(cam, spp, depth, seed=seed, precision=abi.RT_PREC_F64)

@@ -1,6 +1,9 @@
-"""Multi-rank framebuffer partitioning with world_size 2 on
-gloo: the same tile plan and gather bench.py uses, each rank rendering its
-tiles with the oracle, reassembles exactly the single-rank image."""
+"""Multi-rank framebuffer partitioning with world_size 2 on gloo, on the CPU: the
+frame driver bench.py uses (rt_amd.distributed.FrameSharding: the tile plan, the gather to rank 0
+and the scatter) over a stand-in context whose render_tiles writes the oracle's pixels of the tiles
+into the rank's buffer; the gathered frame equals the single-rank image exactly. The same driver on
+librt_hip with both ranks on one GPU: tests/test_gpu_multiprocess.py."""
+import ctypes
 import os
 import socket
 
@@ -16,6 +19,19 @@ def _free_port():
         return s.getsockname()[1]
 
 
+class OracleTiles:
+    """render_tiles of rt_amd.Context (packed tiles into a float64 buffer) computed by the oracle."""
+
+    def __init__(self, oracle, scene):
+        self.oracle, self.scene = oracle, scene
+
+    def render_tiles(self, cam, params, tiles, out_ptr, out_is_device, stream=None):
+        img, _ = self.oracle.render(self.scene, cam, params["spp"], params["depth"], seed=params["seed"],
+                                    tiles=tiles, threads=1)
+        n = img.size
+        ctypes.memmove(out_ptr, img.ctypes.data, n * 8)
+
+
 def _worker(rank, world, port, q):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
@@ -23,22 +39,17 @@ def _worker(rank, world, port, q):
     sys.path[:0] = [os.path.join(repo, "cpu-ray-tracing-implementation_amd", "python"), os.path.join(repo, "oracle")]
     import oracle
     from rt_amd import plugin
-    from rt_amd.tiling import pixel_index, plan
+    from rt_amd.distributed import FrameSharding
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     cs = plugin.ConfigScene("cornell_box", 150)
     W, H = cs.cam.image_width, cs.cam.image_height
-    tiles, counts, maxpix = plan(W, H, world)
-    mine, _ = oracle.render(oracle.from_desc(cs.desc), cs.cam, 2, 6, seed=4, tiles=tiles[rank], threads=1)
-    buf = torch.zeros((maxpix, 3), dtype=torch.float64)
-    buf[:counts[rank]] = torch.from_numpy(mine)
-    parts = [torch.zeros_like(buf) for _ in range(world)] if rank == 0 else None
-    dist.gather(buf, parts, dst=0)
+    shard = FrameSharding(W, H, world, rank, torch.device("cpu"))
+    out, fb = shard.buffers(torch.float64)
+    ctx = OracleTiles(oracle, oracle.from_desc(cs.desc))
+    shard.frame(ctx, cs.cam, {"spp": 2, "depth": 6, "seed": 4}, out, fb, stream=0)
     if rank == 0:
-        fb = np.zeros((H * W, 3))
-        for r in range(world):
-            fb[pixel_index(tiles[r], W)] = parts[r][:counts[r]].numpy()
-        q.put(fb)
+        q.put(fb.numpy())
     dist.barrier()
     dist.destroy_process_group()
 

@@ -1,0 +1,185 @@
+// valu_rates -- issue cost of single VALU opcodes on gfx950 (MI355X), measured.
+//
+// Why: bench.py prices the fp64 headline kernel's VALU issue in SIMD cycles, weighting the fp64
+// add/mul/fma/transcendental instructions (SQ_INSTS_VALU_*_F64) at 4 cycles per wave64 instruction and
+// everything else at 2. The kernel also issues fp64 compares, min/max, conversions, 64-bit moves and
+// 64-bit integer ops, whose costs no document gives. This program measures them: for every opcode a
+// kernel runs 8 independent dependency chains of that one instruction (inline asm) in a loop, with
+// 8 waves on every SIMD, and each wave reads the shader clock around its loop; cycles per wave64
+// instruction per SIMD = wave cycles / (waves per SIMD x instructions per wave).
+// Run under rocprofv3 --pmc as well to see how SQ_INSTS_VALU / SQ_ACTIVE_INST_VALU /
+// SQ_THREAD_CYCLES_VALU count each opcode (scripts/valu_rates.sh).
+//   build: hipcc -O3 --offload-arch=gfx950 -o tools/valu_rates tools/valu_rates.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <vector>
+
+#define CHECK(x)                                                                        \
+  do {                                                                                  \
+    hipError_t e_ = (x);                                                                \
+    if (e_ != hipSuccess) {                                                             \
+      std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));                     \
+      return 1;                                                                         \
+    }                                                                                   \
+  } while (0)
+
+constexpr int kIters = 256;   // loop trips
+constexpr int kPerIter = 64;  // instructions per trip (8 chains x 8)
+
+// one op on chain register r (double / uint64 pairs, float / uint32 singles)
+#define OP8(OP) OP(a0) OP(a1) OP(a2) OP(a3) OP(a4) OP(a5) OP(a6) OP(a7)
+
+template <int K>
+__device__ __forceinline__ void body(double& a0, double& a1, double& a2, double& a3, double& a4, double& a5,
+                                     double& a6, double& a7, double b, float& f0, float& f1, float& f2, float& f3,
+                                     float& f4, float& f5, float& f6, float& f7, float fb, uint64_t& s0, uint64_t& s1,
+                                     uint64_t& s2, uint64_t& s3, uint64_t& s4, uint64_t& s5, uint64_t& s6,
+                                     uint64_t& s7, uint64_t m) {
+#pragma unroll
+  for (int rep = 0; rep < 8; rep++) {
+    if constexpr (K == 0) {
+#define X(r) asm volatile("v_add_f64 %0, %0, %1" : "+v"(r) : "v"(b));
+      OP8(X)
+#undef X
+    } else if constexpr (K == 1) {
+#define X(r) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(r) : "v"(b));
+      OP8(X)
+#undef X
+    } else if constexpr (K == 2) {
+#define X(r) asm volatile("v_fma_f64 %0, %0, %1, %1" : "+v"(r) : "v"(b));
+      OP8(X)
+#undef X
+    } else if constexpr (K == 3) {
+#define X(r) asm volatile("v_max_f64 %0, %0, %1" : "+v"(r) : "v"(b));
+      OP8(X)
+#undef X
+    } else if constexpr (K == 4) {
+#define X(r) { uint64_t t; asm volatile("v_cmp_lt_f64_e64 %0, %1, %2" : "=s"(t) : "v"(a##r), "v"(b)); s##r ^= t; }
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 5) {
+#define X(r) asm volatile("v_mov_b64 %0, %0" : "+v"(r));
+      OP8(X)
+#undef X
+    } else if constexpr (K == 6) {
+#define X(r) asm volatile("v_cvt_f32_f64 %0, %1" : "=v"(f##r) : "v"(a##r));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 7) {
+#define X(r) asm volatile("v_add_f32 %0, %0, %1" : "+v"(f##r) : "v"(fb));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 8) {
+#define X(r) asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(f##r) : "v"(fb));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 9) {
+#define X(r) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(f##r) : "v"(fb), "s"(m));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 10) {
+#define X(r) asm volatile("v_lshl_add_u64 %0, %0, 1, %1" : "+v"(r) : "v"(b));
+      OP8(X)
+#undef X
+    } else if constexpr (K == 11) {
+#define X(r) { uint64_t t; asm volatile("v_cmp_gt_u64_e64 %0, %1, %2" : "=s"(t) : "v"(a##r), "v"(b)); s##r ^= t; }
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 12) {
+#define X(r) asm volatile("v_rcp_f64 %0, %0" : "+v"(r));
+      OP8(X)
+#undef X
+    } else if constexpr (K == 13) {
+#define X(r) asm volatile("v_floor_f64 %0, %0" : "+v"(r));
+      OP8(X)
+#undef X
+    } else if constexpr (K == 14) {
+#define X(r) asm volatile("v_cvt_f64_u32 %0, %1" : "=v"(a##r) : "v"(f##r));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 15) {
+#define X(r) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(f##r) : "v"(fb));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 16) {
+#define X(r) asm volatile("v_ldexp_f64 %0, %0, %1" : "+v"(r) : "v"(fb));
+      OP8(X)
+#undef X
+    } else if constexpr (K == 17) {
+#define X(r) asm volatile("v_lshlrev_b64 %0, 1, %0" : "+v"(r));
+      OP8(X)
+#undef X
+    } else if constexpr (K == 18) {
+#define X(r) asm volatile("v_rsq_f32 %0, %0" : "+v"(f##r));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 19) {
+#define X(r) { uint64_t t; asm volatile("v_cmp_class_f64_e64 %0, %1, %2" : "=s"(t) : "v"(a##r), "v"(f0)); s##r ^= t; }
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    }
+  }
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void k_rate(double* out, unsigned long long* clk, double seed) {
+  double a0 = seed + threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6,
+         a7 = a0 + 7, b = seed * 0.5;
+  float f0 = (float)a0, f1 = (float)a1, f2 = (float)a2, f3 = (float)a3, f4 = (float)a4, f5 = (float)a5,
+        f6 = (float)a6, f7 = (float)a7, fb = (float)b;
+  uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0, s5 = 0, s6 = 0, s7 = 0, m = 0x5555555555555555ull;
+  const unsigned long long t0 = clock64();
+#pragma unroll 1
+  for (int i = 0; i < kIters; i++)
+    body<K>(a0, a1, a2, a3, a4, a5, a6, a7, b, f0, f1, f2, f3, f4, f5, f6, f7, fb, s0, s1, s2, s3, s4, s5, s6, s7, m);
+  const unsigned long long t1 = clock64();
+  if ((threadIdx.x & 63) == 0) clk[blockIdx.x * 4 + (threadIdx.x >> 6)] = t1 - t0;
+  out[blockIdx.x * 256 + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 + f0 + f1 + f2 + f3 + f4 + f5 + f6 +
+                                        f7 + (double)(s0 ^ s1 ^ s2 ^ s3 ^ s4 ^ s5 ^ s6 ^ s7);
+}
+
+struct Entry {
+  const char* name;
+  void (*k)(double*, unsigned long long*, double);
+};
+
+int main() {
+  const Entry es[] = {
+      {"v_add_f64", k_rate<0>},        {"v_mul_f64", k_rate<1>},         {"v_fma_f64", k_rate<2>},
+      {"v_max_f64", k_rate<3>},        {"v_cmp_lt_f64", k_rate<4>},      {"v_mov_b64", k_rate<5>},
+      {"v_cvt_f32_f64", k_rate<6>},    {"v_add_f32", k_rate<7>},         {"v_fma_f32", k_rate<8>},
+      {"v_cndmask_b32", k_rate<9>},    {"v_lshl_add_u64", k_rate<10>},   {"v_cmp_gt_u64", k_rate<11>},
+      {"v_rcp_f64", k_rate<12>},       {"v_floor_f64", k_rate<13>},      {"v_cvt_f64_u32", k_rate<14>},
+      {"v_mul_lo_u32", k_rate<15>},    {"v_ldexp_f64", k_rate<16>},      {"v_lshlrev_b64", k_rate<17>},
+      {"v_rsq_f32", k_rate<18>},       {"v_cmp_class_f64", k_rate<19>},
+  };
+  int ncu = 0;
+  CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+  const int waves_per_simd = 8, blocks = ncu * waves_per_simd;  // 256 lanes = one wave per SIMD per block
+  double* out;
+  unsigned long long* clk;
+  CHECK(hipMalloc(&out, sizeof(double) * blocks * 256));
+  CHECK(hipMalloc(&clk, sizeof(unsigned long long) * blocks * 4));
+  std::vector<unsigned long long> h(blocks * 4);
+  std::printf("{\"cus\": %d, \"waves_per_simd\": %d, \"instr_per_wave\": %d, \"ops\": {", ncu, waves_per_simd,
+              kIters * kPerIter);
+  for (size_t i = 0; i < sizeof(es) / sizeof(es[0]); i++) {
+    for (int rep = 0; rep < 2; rep++) {  // the first launch warms up
+      hipLaunchKernelGGL(es[i].k, dim3(blocks), dim3(256), 0, 0, out, clk, 1.25);
+      CHECK(hipGetLastError());
+      CHECK(hipDeviceSynchronize());
+    }
+    CHECK(hipMemcpy(h.data(), clk, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+    double mean = 0;
+    for (auto c : h) mean += (double)c;
+    mean /= (double)h.size();
+    const double cpi = mean / ((double)waves_per_simd * kIters * kPerIter);
+    std::printf("%s\"%s\": %.3f", i ? ", " : "", es[i].name, cpi);
+  }
+  std::printf("}, \"unit\": \"shader-clock cycles per wave64 instruction per SIMD (8 waves/SIMD, 8 chains)\"}\n");
+  CHECK(hipFree(out));
+  CHECK(hipFree(clk));
+  return 0;
+}
