@@ -117,7 +117,30 @@ __device__ __forceinline__ double flog(double x) { return log(x); }
 // Payne-Hanek path: OCML's general sin/cos carry one, whose registers (the kernel's budget is its
 // heaviest path) held the fp64 kernels at 2-3 waves per SIMD. Within an ulp or two of
 // sin(fl(2 pi u)): far inside the fp64 parity tolerance (1e-9 relative against the oracle).
-__device__ __forceinline__ void sincos2pi(double u, double& s, double& c) { sincospi(2.0 * u, &s, &c); }
+// Round 4: a 1024-entry table of (sin, cos)(2 pi j / 1024), correctly rounded on the host (rt_kernels.hip
+// sincos_table_init), and the angle addition formulas for the rest, delta = 2 pi (u - j / 1024) < 2 pi / 1024:
+// sin delta = delta (1 - delta^2 / 6 + delta^4 / 120) and cos delta - 1 = delta^2 (-1/2 + delta^2 / 24 -
+// delta^4 / 720) leave truncation errors below 1e-19, so the result is within about an ulp, like
+// OCML's sincospi, at one table read and 13 fp64 operations instead of ~22 fp64 and ~20 other VALU
+// operations (and the polynomial constants OCML's version kept in 18 VGPRs across the path loop).
+// u * 1024 and its fractional part are exact for every double u in [0, 1).
+constexpr int kSinCosTab = 1024;
+__device__ double2 g_sincos_tab[kSinCosTab];
+__device__ __forceinline__ void sincos2pi(double u, double& s, double& c) {
+#ifdef RT_OCML_SINCOS
+  sincospi(2.0 * u, &s, &c);
+#else
+  const double t = u * double(kSinCosTab);
+  const double h = floor(t);
+  const double2 sc = g_sincos_tab[(uint32_t)(int32_t)h & (kSinCosTab - 1)];
+  const double d = (t - h) * (2.0 * 3.14159265358979323846 / kSinCosTab);
+  const double d2 = d * d;
+  const double sd = d * fma(d2, fma(d2, 1.0 / 120.0, -1.0 / 6.0), 1.0);
+  const double cm1 = d2 * fma(d2, fma(d2, -1.0 / 720.0, 1.0 / 24.0), -0.5);
+  s = fma(sc.y, sd, fma(sc.x, cm1, sc.x));
+  c = fma(-sc.x, sd, fma(sc.y, cm1, sc.y));
+#endif
+}
 // x / pi (pdf.h:27-29 cosine_pdf::value): fp32 as before, fp64 as a product with 1/pi
 __device__ __forceinline__ float div_pi(float x) { return fdiv(x, 3.14159265358979323846f); }
 __device__ __forceinline__ double div_pi(double x) { return x * 0.318309886183790671537767526745; }

@@ -58,6 +58,12 @@ constexpr int kBlock = 256;
 #ifndef RT_COLD_LDS  // the volume linear program: the cold path state in LDS (Path, LC)
 #define RT_COLD_LDS 1
 #endif
+#ifndef RT_COLD_LDS_F64  // the same for the fp64 volume program (round 4)
+#define RT_COLD_LDS_F64 1
+#endif
+#ifndef RT_LINEAR_NORAD  // the volume programs: emission added straight into the item's running sum (Path NORAD)
+#define RT_LINEAR_NORAD 1
+#endif
 #ifndef RT_F64_TAIL  // 1: fp64 renders use the fp32 item layout (bulk + tail items); 0: uniform items of 16
 #define RT_F64_TAIL 1
 #endif
@@ -211,8 +217,15 @@ __device__ __forceinline__ __attribute__((unused)) double* cold_acc64() {
 // running sum, its pixel and RNG key, the sample counter and range, the fp64 camera base -- are
 // registers too unless LC, where they live in the lane's LDS words (cold_words) so the trace and
 // shade code of the persistent loop gets their 14 VGPRs.
-template <class R, bool LC = false>
+// LEAN: the pixel key, the end of the item's sample range and the camera base are not kept at all but
+// recomputed where they are used (ka_of, send_of, begin_sample): 8 fewer registers for kernels whose
+// traversal state competes with them (the wide BVH kernels), at a few integer and fp64 operations per
+// sample.
+// NORAD: no radiance register either (shade adds emission straight into the item's running sum).
+template <class R, bool LC = false, bool LEAN = false, bool NORAD = LEAN>
 struct Path {
+  static constexpr bool kLean = LEAN;
+  static constexpr bool kNoRad = NORAD;
   V<R> o, d, thr, rad;
   R tm;
   int32_t bounce;
@@ -286,8 +299,10 @@ static_assert(Path<float>::kXy < kColdWords, "cold words");
 template <class R, class PS>
 __device__ __forceinline__ void pixel_base(const Params<R>& p, PS& s, uint32_t xy) {
 #if RT_CAM_BASE
-  const double x = double(xy & 0xFFFFu), y = double(xy >> 16);
-  s.set_cb((ld_here(&p.camx->dir00) + x * ld_here(&p.camx->du)) + y * ld_here(&p.camx->dv));
+  if constexpr (!PS::kLean) {
+    const double x = double(xy & 0xFFFFu), y = double(xy >> 16);
+    s.set_cb((ld_here(&p.camx->dir00) + x * ld_here(&p.camx->du)) + y * ld_here(&p.camx->dv));
+  }
 #endif
 }
 
@@ -386,20 +401,52 @@ __device__ __forceinline__ uint32_t next_item_dyn(const Params<R>& p) {
   return item;
 }
 
-// A new work item for the slot: its pixel and that pixel's RNG key.
-template <class R, class PS>
-__device__ __forceinline__ void begin_item(const Params<R>& p, PS& s, uint32_t item) {
-  const uint32_t chunk = (uint32_t)(((uint64_t)item * p.npix_m) >> p.npix_k);
-  const uint32_t xy = p.pixmap[item - chunk * p.npix];
+// An item's first sample and the end of its sample range: bulk items of p.chunk samples, then tail
+// items of p.tail_chunk (the item layout, render())
+template <class R>
+__device__ __forceinline__ void item_range(const Params<R>& p, uint32_t item, uint32_t& chunk, uint32_t& first,
+                                           uint32_t& end) {
+  chunk = (uint32_t)(((uint64_t)item * p.npix_m) >> p.npix_k);
   // fp64 items are uniform (the host never gives them a tail): compiled out, the select costs
   // the fp64 Cornell kernel 10 VGPRs, 3 -> 2 waves per SIMD (C2 f64 5.22 -> 4.08 Gsamples/s)
   const bool bulk = (sizeof(R) == 8 && !RT_F64_TAIL) || chunk < p.k_bulk;
-  const uint32_t first = bulk ? chunk * p.chunk : p.k_bulk * p.chunk + (chunk - p.k_bulk) * p.tail_chunk;
+  first = bulk ? chunk * p.chunk : p.k_bulk * p.chunk + (chunk - p.k_bulk) * p.tail_chunk;
+  end = min(first + (bulk ? p.chunk : p.tail_chunk), p.spp);
+}
+// the pixel's RNG key and the end of the item's samples: kept, or (LEAN) recomputed
+template <class R, class PS>
+__device__ __forceinline__ uint32_t ka_of(const Params<R>& p, const PS& s) {
+  if constexpr (PS::kLean) {
+    const uint32_t xy = s.xy();
+    return key_pixel(p.seed, (xy >> 16) * p.W + (xy & 0xFFFFu));
+  } else {
+    return s.ka();
+  }
+}
+template <class R, class PS>
+__device__ __forceinline__ uint32_t send_of(const Params<R>& p, const PS& s) {
+  if constexpr (PS::kLean) {
+    uint32_t chunk, first, end;
+    item_range(p, s.item(), chunk, first, end);
+    return end;
+  } else {
+    return s.send();
+  }
+}
+
+// A new work item for the slot: its pixel and that pixel's RNG key.
+template <class R, class PS>
+__device__ __forceinline__ void begin_item(const Params<R>& p, PS& s, uint32_t item) {
+  uint32_t chunk, first, end;
+  item_range(p, item, chunk, first, end);
+  const uint32_t xy = p.pixmap[item - chunk * p.npix];
   s.set_item(item);
   s.set_sample(first);
-  s.set_send(min(first + (bulk ? p.chunk : p.tail_chunk), p.spp));
   s.set_xy(xy);
-  s.set_ka(key_pixel(p.seed, (xy >> 16) * p.W + (xy & 0xFFFFu)));
+  if constexpr (!PS::kLean) {
+    s.set_send(end);
+    s.set_ka(key_pixel(p.seed, (xy >> 16) * p.W + (xy & 0xFFFFu)));
+  }
   pixel_base(p, s, xy);
 }
 
@@ -450,7 +497,7 @@ __device__ __forceinline__ void camera_ray(const CamDev* cp, uint32_t ks, uint32
 // camera::generate_ray, perspective mode (camera.h:244-251,293): sample s.sample of the slot's pixel
 template <class R, bool CAMX, class PS>
 __device__ __forceinline__ void begin_sample(const Params<R>& p, PS& s) {
-  s.ks = key_path(s.ka(), key_sample(p.seed, p.first_sample + s.sample()));
+  s.ks = key_path(ka_of(p, s), key_sample(p.seed, p.first_sample + s.sample()));
   // In fp64 for both paths: fp32 gets the correctly rounded ray, a few ulp less error on every
   // camera ray, which otherwise shows up as paths crossing a checker line or edge differently.
   const double ox = to_unit<double>(draw_u32(s.ks, 0)) - 0.5;  // sample_square (camera.h:293)
@@ -459,12 +506,12 @@ __device__ __forceinline__ void begin_sample(const Params<R>& p, PS& s) {
   double tm;
   if (!CAMX || p.cam_mode == RT_CAM_PERSPECTIVE) {  // camera.h:245-251
     const V<double> du = ld_here(&p.camx->du), dv = ld_here(&p.camx->dv);
-#if RT_CAM_BASE
-    d = (s.cb() + ox * du) + oy * dv;
-#else
-    const uint32_t xy = s.xy(), x = xy & 0xFFFFu, y = xy >> 16;
-    d = ((ld_here(&p.camx->dir00) + double(x) * du) + double(y) * dv + ox * du) + oy * dv;
-#endif
+    if constexpr (RT_CAM_BASE && !PS::kLean) {
+      d = (s.cb() + ox * du) + oy * dv;
+    } else {  // the same operations in the same order as pixel_base + the above: bit-identical
+      const uint32_t xy = s.xy(), x = xy & 0xFFFFu, y = xy >> 16;
+      d = ((ld_here(&p.camx->dir00) + double(x) * du) + double(y) * dv + ox * du) + oy * dv;
+    }
     tm = to_unit<double>(draw_u32(s.ks, 2));
   } else if constexpr (CAMX) {
     const uint32_t xy = s.xy();
@@ -475,7 +522,7 @@ __device__ __forceinline__ void begin_sample(const Params<R>& p, PS& s) {
   s.tm = R(tm);
   s.bounce = 0;
   s.thr = mkv(R(1), R(1), R(1));
-  s.rad = mkv(R(0), R(0), R(0));
+  if constexpr (!PS::kNoRad) s.rad = mkv(R(0), R(0), R(0));
   s.xe = kNoHit;
   s.xi = -1;
 }
@@ -503,7 +550,11 @@ __global__ __launch_bounds__(kBlock) void k_init(Params<R> p) {
 // has no work left.
 // FLAT: the hit comes from the flat program (trace_flat): a quad whose outward normal (+-e_A)
 // and material are packed in nm, so no primitive or instance record is read.
-template <class R, bool CAMX, bool FLAT = false, class PS>
+// MOVING = false: the kernel's scene has no moving sphere (the wide kernels without WK_MOVING), so the
+// ray time is not read here. A LEAN path has no radiance register: emission goes straight into the
+// item's running sum (the same terms, added one by one instead of per sample: a rounding-level
+// regrouping of the pixel's sum).
+template <class R, bool CAMX, bool FLAT = false, bool MOVING = true, class PS>
 __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, uint32_t nm = 0) {
   const DevScene<R>& sc = p.sc;
   V<R> add = mkv(R(0), R(0), R(0));
@@ -576,7 +627,7 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
         }
       } else if (ty == E_SPHERE) {  // sphere.h:69 (center_ member; (0,0,0) for moving spheres)
         const Sphere<R>& sp = sc.spheres[idx];
-        unit_n = !sp.moving;
+        unit_n = !MOVING || !sp.moving;
         if constexpr (sizeof(R) == 8) {
           outward = (po - ld3(sp.cn)) / sp.r;
         } else {
@@ -758,7 +809,12 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
       if (s.thr.x == R(0) && s.thr.y == R(0) && s.thr.z == R(0)) done = true;
     }
   }
-  if (has_add) s.rad = s.rad + add;
+  if (has_add) {
+    if constexpr (PS::kNoRad)
+      s.set_acc(s.acc() + add);
+    else
+      s.rad = s.rad + add;
+  }
   if (!done) {
     s.o = new_o;
     s.d = new_d;
@@ -769,10 +825,11 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
   }
   // the sample is finished (camera.h:167): add it to the item's running sum
   RT_WIDE_STAT(8);
-  const V<R> acc = s.acc() + s.rad;
+  V<R> acc = s.acc();
+  if constexpr (!PS::kNoRad) acc = acc + s.rad;
   const uint32_t sample = s.sample() + 1;
   s.set_sample(sample);
-  if (sample < s.send()) {
+  if (sample < send_of(p, s)) {
     s.set_acc(acc);
   } else {
     const uint32_t item = s.item();
@@ -809,7 +866,9 @@ struct LinearTrav {
   static constexpr bool kFlat = false;
   static constexpr bool kWide = false;
   // the volume program's registers (C5: 23 -> 6 VGPRs spilled at 96, 1563 -> 1498 ms/frame)
-  static constexpr bool kColdLds = sizeof(R) == 4 && VOL && RT_COLD_LDS;
+  static constexpr bool kLean = false;
+  static constexpr bool kNoRad = VOL && RT_LINEAR_NORAD;
+  static constexpr bool kColdLds = VOL && (sizeof(R) == 4 ? RT_COLD_LDS : RT_COLD_LDS_F64);
   template <class PS>
   __device__ __forceinline__ static void run(const DevScene<R>& sc, const Node<R>*, const PS& s, Keys k,
                                              uint32_t*, R& t, uint32_t& e, int32_t& i, uint32_t&) {
@@ -823,6 +882,9 @@ struct LinearTrav {
 #ifndef RT_F64_COLD_LDS  // fp64 flat program: the cold path state (item sum, pixel, keys, camera base) in LDS
 #define RT_F64_COLD_LDS 1
 #endif
+#ifndef RT_FLAT_NORAD  // flat program: emission added straight into the item's running sum (Path NORAD)
+#define RT_FLAT_NORAD 1
+#endif
 #ifndef RT_FLAT_WAVES_F64  // fp64 flat program: waves per SIMD the register budget is cut for (1: none)
 #define RT_FLAT_WAVES_F64 4
 #endif
@@ -834,6 +896,8 @@ struct FlatTrav {
   static constexpr bool kFlat = true;
   static constexpr bool kWide = false;
   // fp32: 72 -> 64 VGPRs, but C2 23.5 -> 24.1 ms/frame; fp64: see RT_F64_COLD_LDS
+  static constexpr bool kLean = false;
+  static constexpr bool kNoRad = RT_FLAT_NORAD;  // 6 VGPRs in fp64 (its item sum is in LDS)
   static constexpr bool kColdLds = sizeof(R) == 8 && RT_F64_COLD_LDS;
   template <class PS>
   __device__ __forceinline__ static void run(const DevScene<R>& sc, const Node<R>*, const PS& s, Keys, uint32_t*,
@@ -851,6 +915,8 @@ struct StackTrav {
   static constexpr int kWaves = sizeof(R) == 4 ? RT_STACK_WAVES : (LDSN ? 1 : RT_STACK_WAVES_F64);  // occupancy over a small spill
   static constexpr bool kFlat = false;
   static constexpr bool kWide = false;
+  static constexpr bool kLean = false;
+  static constexpr bool kNoRad = false;
   static constexpr bool kColdLds = false;  // its LDS holds the traversal stacks
   template <class PS>
   __device__ __forceinline__ static void run(const DevScene<R>& sc, const Node<R>* nodes, const PS& s, Keys k,
@@ -892,6 +958,9 @@ struct StackTrav {
 #ifndef RT_WIDE_WAVES_GLOBAL_F64  // tree in HBM (C4 fp64: 3 waves 599.8, 4: 555.0, 5: 567.3)
 #define RT_WIDE_WAVES_GLOBAL_F64 4
 #endif
+#ifndef RT_WIDE_LEAN  // the wide kernels keep the lean path state (Path LEAN)
+#define RT_WIDE_LEAN 1
+#endif
 template <class R, bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN>
 struct WideTrav {
   static constexpr int kStack = 0;
@@ -901,6 +970,9 @@ struct WideTrav {
   static constexpr bool kFlat = false;
   static constexpr bool kWide = true;
   static constexpr bool kColdLds = false;  // its LDS holds the tree and the stacks
+  static constexpr bool kLean = RT_WIDE_LEAN;  // registers for the traversal (fewer spills)
+  static constexpr bool kNoRad = RT_WIDE_LEAN;
+  static constexpr bool kMoving = MOV;
   using StackT = WStackT<LDSN>;
   using WW = typename WWord<R>::T;
   // LDS layout: [nodes, kWNodeLdsStride each][primitive words][stack: entries x kBlock of StackT]
@@ -1057,7 +1129,7 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
   }
   uint64_t segs = 0;
   if (item0 < p.n_items) {
-    Path<R, Trav::kColdLds> s;
+    Path<R, Trav::kColdLds, Trav::kLean, Trav::kNoRad> s;
     s.set_acc(mkv(R(0), R(0), R(0)));
     begin_item(p, s, item0);
     begin_sample<R, CAMX>(p, s);
@@ -1098,12 +1170,12 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
 #ifdef RT_SECTION_CLOCKS
         RT_WIDE_STAT(4);
         const uint64_t c1 = clock64();
-        const bool more = shade<R, CAMX, false>(q, s, t, e, -1, 0);
+        const bool more = shade<R, CAMX, false, Trav::kMoving>(q, s, t, e, -1, 0);
         if (__lane_id() == (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1)
           atomicAdd(wide_stats_lds() + 7, (unsigned long long)(clock64() - c1));
         if (!more) break;
 #else
-        if (!shade<R, CAMX, false>(q, s, t, e, -1, 0)) break;
+        if (!shade<R, CAMX, false, Trav::kMoving>(q, s, t, e, -1, 0)) break;
 #endif
       }
     } else {
@@ -1594,8 +1666,23 @@ void launch_k(const Params<R>& p, uint32_t grid, hipStream_t st) {
   }
 }
 
+// RT_DEV_ONLY (development builds for register/spill iteration, scripts/kernel_usage.py): instantiate
+// one kernel family only -- 1 the flat program, 2 the wide BVH, 3 the linear programs. 0: everything.
+#ifndef RT_DEV_ONLY
+#define RT_DEV_ONLY 0
+#endif
 template <class R>
 void launch_step(const Params<R>& p, int stack, bool sph, bool tri, uint32_t grid, hipStream_t st) {
+#if RT_DEV_ONLY == 1
+  launch_k<R, FlatTrav<R>>(p, grid, st);
+  return;
+#elif RT_DEV_ONLY == 2
+  launch_wide(p, grid, st);
+  return;
+#elif RT_DEV_ONLY == 3
+  launch_k<R, LinearTrav<R, false, false, true>>(p, grid, st);
+  return;
+#else
   const bool vol = p.sc.has_volumes != 0;
   // the flat program (world-space quads and boxes, fp32 and fp64); the extended kernels keep the linear one
   if (p.sc.has_flat && p.cam_mode == RT_CAM_PERSPECTIVE && !p.sc.has_procedural) {
@@ -1632,6 +1719,7 @@ void launch_step(const Params<R>& p, int stack, bool sph, bool tri, uint32_t gri
   } else {
     launch_k<R, StackTrav<R, kStackDepth>>(p, grid, st);
   }
+#endif
 }
 
 template <class R>
@@ -1901,6 +1989,23 @@ extern "C" {
 
 int32_t rt_abi_version(void) { return RT_ABI_VERSION; }
 
+namespace {
+// g_sincos_tab (rt_device.h sincos2pi, fp64): (sin, cos)(2 pi j / 1024) in long double, rounded once,
+// copied to the device of the calling thread (every context's device; module globals are per device)
+hipError_t sincos_table_init() {
+  static double2 tab[kSinCosTab];
+  static std::once_flag once;
+  std::call_once(once, [] {
+    const long double pi = 3.141592653589793238462643383279502884L;
+    for (int j = 0; j < kSinCosTab; j++) {
+      const long double a = 2.0L * pi * (long double)j / (long double)kSinCosTab;
+      tab[j] = make_double2((double)sinl(a), (double)cosl(a));
+    }
+  });
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_sincos_tab), tab, sizeof(tab));
+}
+}  // namespace
+
 rt_status rt_context_create(int32_t device, rt_context** out) {
   if (!out) return set_err(nullptr, RT_ERR_INVALID_ARGUMENT, "out is null");
   *out = nullptr;
@@ -1912,6 +2017,8 @@ rt_status rt_context_create(int32_t device, rt_context** out) {
   }
   if (device < 0 || device >= n) return set_err(nullptr, RT_ERR_INVALID_ARGUMENT, "device index out of range");
   if ((e = hipSetDevice(device)) != hipSuccess) return set_err(nullptr, RT_ERR_HIP, hipGetErrorString(e));
+  if ((e = sincos_table_init()) != hipSuccess)
+    return set_err(nullptr, RT_ERR_HIP, std::string("sin/cos table: ") + hipGetErrorString(e));
   auto* c = new rt_context;
   c->device = device;
   if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
