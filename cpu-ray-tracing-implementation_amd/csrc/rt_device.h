@@ -329,6 +329,7 @@ struct DevScene {
   const FlatQuadT<R>* flatq;  // flat program (has_flat): quads grouped by plane axis, then boxes
   const FlatBoxT<R>* flatb;
   uint32_t n_flatq[3], n_flatb;
+  uint32_t n_mats;
   int32_t has_flat;
   uint32_t root;
   int32_t background;
@@ -1481,9 +1482,11 @@ __device__ __forceinline__ Slab<R> flat_slab(const FlatBoxT<R>& b, V<R> o, V<R> 
   s.th = s.tn >= tmin ? s.tn : s.tf;
   return s;
 }
+// fq / fb: where the hit's record is read at the end (the scene's, or the kernel's LDS copy)
 template <class R>
 __device__ __forceinline__ void trace_flat(const DevScene<R>& sc, V<R> o, V<R> d, uint32_t excl_e, int32_t excl_i,
-                                           R& t_best, uint32_t& e_best, int32_t& i_best, uint32_t& nm) {
+                                           R& t_best, uint32_t& e_best, int32_t& i_best, uint32_t& nm,
+                                           const FlatQuadT<R>* fq, const FlatBoxT<R>* fb) {
   const R tmin = R(0.001);
   R tmax = Num<R>::inf();
   const V<R> inv = flat_inv(d);
@@ -1508,7 +1511,7 @@ __device__ __forceinline__ void trace_flat(const DevScene<R>& sc, V<R> o, V<R> d
   nm = 0;
   if (best < 0) return;
   if ((uint32_t)best < nq) {
-    const FlatQuadT<R>& r = sc.flatq[best];
+    const FlatQuadT<R>& r = fq[best];
     e_best = r.e;
     i_best = r.inst;
     nm = r.nm;
@@ -1516,7 +1519,7 @@ __device__ __forceinline__ void trace_flat(const DevScene<R>& sc, V<R> o, V<R> d
   }
   // the face of the box: the axis whose slab bound is the hit distance (recomputed exactly
   // as in the loop), on the side the ray enters (or leaves, from inside)
-  const FlatBoxT<R>& b = sc.flatb[(uint32_t)best - nq];
+  const FlatBoxT<R>& b = fb[(uint32_t)best - nq];
   const Slab<R> s = flat_slab(b, o, inv, tmin, excl_i, xf);
   const bool enter = s.tn >= tmin;
   int k = 2;

@@ -555,7 +555,8 @@ __global__ __launch_bounds__(kBlock) void k_init(Params<R> p) {
 // item's running sum (the same terms, added one by one instead of per sample: a rounding-level
 // regrouping of the pixel's sum).
 template <class R, bool CAMX, bool FLAT = false, bool MOVING = true, class PS>
-__device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, uint32_t nm = 0) {
+__device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, uint32_t nm = 0,
+                      const Material<R>* mats = nullptr) {
   const DevScene<R>& sc = p.sc;
   V<R> add = mkv(R(0), R(0), R(0));
   bool has_add = false, done = false;
@@ -694,7 +695,7 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
            (double)d.z, (double)t, (double)pw.x, (double)pw.y, (double)pw.z, (double)n.x, (double)n.y, (double)n.z,
            (int)front, sc.mats[mat].kind, ty, idx);
 #endif
-    const Material<R>& m = sc.mats[mat];
+    const Material<R>& m = (mats ? mats : sc.mats)[mat];
     if (m.kind == M_DIFFUSE_LIGHT) {  // material.h:211-215; no scatter
       if (front) {
         add = s.thr * tex_sample<R, CAMX>(sc, m.tx, pw, hu, hv);
@@ -866,6 +867,7 @@ struct LinearTrav {
   static constexpr bool kFlat = false;
   static constexpr bool kWide = false;
   // the volume program's registers (C5: 23 -> 6 VGPRs spilled at 96, 1563 -> 1498 ms/frame)
+  static constexpr bool kTablesLds = false;
   static constexpr bool kLean = false;
   static constexpr bool kNoRad = VOL && RT_LINEAR_NORAD;
   static constexpr bool kColdLds = VOL && (sizeof(R) == 4 ? RT_COLD_LDS : RT_COLD_LDS_F64);
@@ -882,14 +884,18 @@ struct LinearTrav {
 #ifndef RT_F64_COLD_LDS  // fp64 flat program: the cold path state (item sum, pixel, keys, camera base) in LDS
 #define RT_F64_COLD_LDS 1
 #endif
+#ifndef RT_FLAT_LDS  // flat program (persistent kernels): records and materials copied into LDS
+#define RT_FLAT_LDS 1
+#endif
 #ifndef RT_FLAT_NORAD  // flat program: emission added straight into the item's running sum (Path NORAD)
 #define RT_FLAT_NORAD 1
 #endif
 #ifndef RT_FLAT_WAVES_F64  // fp64 flat program: waves per SIMD the register budget is cut for (1: none)
 #define RT_FLAT_WAVES_F64 4
 #endif
-template <class R>
+template <class R, bool TLDS = false>
 struct FlatTrav {
+  static constexpr bool kTablesLds = TLDS;  // persistent kernel: Tables in LDS (fill, run_lds)
   static constexpr int kStack = 0;
   static constexpr int kWaves = sizeof(R) == 4 ? RT_FLAT_WAVES : RT_FLAT_WAVES_F64;
   static constexpr int kLdsNodes = 0;
@@ -902,7 +908,30 @@ struct FlatTrav {
   template <class PS>
   __device__ __forceinline__ static void run(const DevScene<R>& sc, const Node<R>*, const PS& s, Keys, uint32_t*,
                                              R& t, uint32_t& e, int32_t& i, uint32_t& nm) {
-    trace_flat<R>(sc, s.o, s.d, s.xe, s.xi, t, e, i, nm);
+    trace_flat<R>(sc, s.o, s.d, s.xe, s.xi, t, e, i, nm, sc.flatq, sc.flatb);
+  }
+  // the scene's small tables copied into LDS (persistent kernel, RT_FLAT_LDS): the hit's record and
+  // material are then LDS reads instead of dependent global loads
+  static constexpr uint32_t kLdsQuads = 64, kLdsBoxes = 16, kLdsMats = 32;
+  struct Tables {
+    FlatQuadT<R> q[kLdsQuads];
+    FlatBoxT<R> b[kLdsBoxes];
+    Material<R> m[kLdsMats];
+  };
+  __host__ __device__ __forceinline__ static bool tables_fit(const DevScene<R>& sc) {
+    return sc.n_flatq[0] + sc.n_flatq[1] + sc.n_flatq[2] <= kLdsQuads && sc.n_flatb <= kLdsBoxes &&
+           sc.n_mats <= kLdsMats;
+  }
+  __device__ __forceinline__ static void fill(const DevScene<R>& sc, Tables& tb) {
+    const uint32_t nq = sc.n_flatq[0] + sc.n_flatq[1] + sc.n_flatq[2];
+    for (uint32_t j = threadIdx.x; j < nq; j += kBlock) tb.q[j] = sc.flatq[j];
+    for (uint32_t j = threadIdx.x; j < sc.n_flatb; j += kBlock) tb.b[j] = sc.flatb[j];
+    for (uint32_t j = threadIdx.x; j < sc.n_mats; j += kBlock) tb.m[j] = sc.mats[j];
+  }
+  template <class PS>
+  __device__ __forceinline__ static void run_lds(const DevScene<R>& sc, const Tables& tb, const PS& s, R& t,
+                                                 uint32_t& e, int32_t& i, uint32_t& nm) {
+    trace_flat<R>(sc, s.o, s.d, s.xe, s.xi, t, e, i, nm, tb.q, tb.b);
   }
 };
 // LDSN: the scene's BVH nodes (at most kLdsNodeMax) are copied into LDS at kernel start, so
@@ -915,6 +944,7 @@ struct StackTrav {
   static constexpr int kWaves = sizeof(R) == 4 ? RT_STACK_WAVES : (LDSN ? 1 : RT_STACK_WAVES_F64);  // occupancy over a small spill
   static constexpr bool kFlat = false;
   static constexpr bool kWide = false;
+  static constexpr bool kTablesLds = false;
   static constexpr bool kLean = false;
   static constexpr bool kNoRad = false;
   static constexpr bool kColdLds = false;  // its LDS holds the traversal stacks
@@ -970,6 +1000,7 @@ struct WideTrav {
   static constexpr bool kFlat = false;
   static constexpr bool kWide = true;
   static constexpr bool kColdLds = false;  // its LDS holds the tree and the stacks
+  static constexpr bool kTablesLds = false;
   static constexpr bool kLean = RT_WIDE_LEAN;  // registers for the traversal (fewer spills)
   static constexpr bool kNoRad = RT_WIDE_LEAN;
   static constexpr bool kMoving = MOV;
@@ -1098,6 +1129,15 @@ __device__ __forceinline__ void step_body(const Params<R>& p) {
 // one counter for the whole chip serialised across the 8 XCDs' L2s: measured 6x slower on C2).
 // Static (persist 1): lanes walk items lane, lane + P, ... (P = grid lanes). No state goes
 // through HBM between segments, there is no launch per K segments and no live-slot compaction.
+// Trav::Tables for the flat program, an empty stand-in for the others
+template <class R, class Trav, bool = Trav::kTablesLds>
+struct FlatTables {
+  struct T {};
+};
+template <class R, class Trav>
+struct FlatTables<R, Trav, true> {
+  using T = typename Trav::Tables;
+};
 template <class R, class Trav, bool CAMX>
 __device__ __forceinline__ void persist_body(const Params<R>& p) {
   __shared__ Lds<Trav::kStack * kBlock> stk;
@@ -1118,6 +1158,13 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
     extern __shared__ uint4 dyn_lds[];
     wstk = Trav::fill(p.sc, dyn_lds) + threadIdx.x;
     trav_nodes = (const Node<R>*)dyn_lds;
+  }
+  [[maybe_unused]] const typename FlatTables<R, Trav>::T* flat_tb = nullptr;
+  if constexpr (Trav::kTablesLds) {  // the host launches this kernel only when the tables fit
+    __shared__ typename FlatTables<R, Trav>::T tb;
+    Trav::fill(p.sc, tb);
+    __syncthreads();
+    flat_tb = &tb;
   }
   uint32_t item0 = blockIdx.x * kBlock + threadIdx.x;
   if (p.persist == 2) {
@@ -1177,6 +1224,26 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
 #else
         if (!shade<R, CAMX, false, Trav::kMoving>(q, s, t, e, -1, 0)) break;
 #endif
+      }
+    } else if constexpr (Trav::kTablesLds) {
+      // the flat program with its records and materials in LDS (Trav::Tables); the parameters are
+      // reloaded per segment as below
+      using KP = const __attribute__((address_space(4))) Params<R>*;
+      const KP kp0 = (KP)__builtin_amdgcn_kernarg_segment_ptr();
+#pragma unroll 1
+      for (;;) {
+        KP kp = kp0;
+        asm volatile("" : "+s"(kp));
+        const Params<R>& q = *(const Params<R>*)kp;
+        R t;
+        uint32_t e, nm = 0;
+        int32_t inst;
+        Trav::run_lds(q.sc, *flat_tb, s, t, e, inst, nm);
+        if (++segs > q.seg_cap) {  // cannot happen: every segment advances a bounce-capped path
+          atomicOr(q.fault, 1u);
+          break;
+        }
+        if (!shade<R, CAMX, true>(q, s, t, e, inst, nm, flat_tb->m)) break;
       }
     } else {
 #if RT_PARAM_RELOAD
@@ -1551,6 +1618,7 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
   s.flatb = (const FlatBoxT<R>*)at(h.off_flat_box);
   for (int a = 0; a < 3; a++) s.n_flatq[a] = h.n_flat_quad[a];
   s.n_flatb = h.n_flat_box;
+  s.n_mats = h.n_mats;
   s.root = h.root;
   s.background = h.background;
   s.has_volumes = h.has_volumes;
@@ -1674,7 +1742,10 @@ void launch_k(const Params<R>& p, uint32_t grid, hipStream_t st) {
 template <class R>
 void launch_step(const Params<R>& p, int stack, bool sph, bool tri, uint32_t grid, hipStream_t st) {
 #if RT_DEV_ONLY == 1
-  launch_k<R, FlatTrav<R>>(p, grid, st);
+  if (RT_FLAT_LDS && p.persist && FlatTrav<R, true>::tables_fit(p.sc))
+    launch_k<R, FlatTrav<R, true>>(p, grid, st);
+  else
+    launch_k<R, FlatTrav<R>>(p, grid, st);
   return;
 #elif RT_DEV_ONLY == 2
   launch_wide(p, grid, st);
@@ -1686,7 +1757,10 @@ void launch_step(const Params<R>& p, int stack, bool sph, bool tri, uint32_t gri
   const bool vol = p.sc.has_volumes != 0;
   // the flat program (world-space quads and boxes, fp32 and fp64); the extended kernels keep the linear one
   if (p.sc.has_flat && p.cam_mode == RT_CAM_PERSPECTIVE && !p.sc.has_procedural) {
-    launch_k<R, FlatTrav<R>>(p, grid, st);
+    if (RT_FLAT_LDS && p.persist && FlatTrav<R, true>::tables_fit(p.sc))
+      launch_k<R, FlatTrav<R, true>>(p, grid, st);
+    else
+      launch_k<R, FlatTrav<R>>(p, grid, st);
     return;
   }
   if (p.sc.n_linear > 0) {
