@@ -33,6 +33,9 @@ namespace rtd {
 #ifndef RT_WIDE_PREFETCH  // a triangle's words loaded with the record's first word (C4 358.9 -> 357.2 ms)
 #define RT_WIDE_PREFETCH 1
 #endif
+#ifndef RT_WIDE_OCTPACK
+#define RT_WIDE_OCTPACK 1
+#endif
 
 // Math policy. fp64 (the parity path): libm where the reference calls it (log), and division,
 // reciprocal and square root refined from the hardware estimates to about an ulp (below).
@@ -1065,8 +1068,12 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
   // save (C4 fp32 351 -> 460 ms/frame; fp64 C3 89.8 -> 81.7, C4 561 -> 545), so fp32 keeps
   // (p - o) * inv, octant-ordered (RT_WIDE_OCT32: C3 fp32 60.9 -> 57.2, C4 351.9 -> 341.6).
   constexpr bool kFma = F64 && RT_WIDE_FMA, kOct = kFma || (!F64 && RT_WIDE_OCT32);
-  [[maybe_unused]] const uint32_t onx = (__float_as_uint(inv.x) >> 31) * 48u, ony = 16u + (__float_as_uint(inv.y) >> 31) * 48u,
-                 onz = 32u + (__float_as_uint(inv.z) >> 31) * 48u;
+  [[maybe_unused]] const uint32_t onx0 = (__float_as_uint(inv.x) >> 31) * 48u,
+                                 ony0 = 16u + (__float_as_uint(inv.y) >> 31) * 48u,
+                                 onz0 = 32u + (__float_as_uint(inv.z) >> 31) * 48u;
+  // RT_WIDE_OCTPACK: the three near-plane offsets packed in one register and unpacked per node visit
+  // (three bit-field extracts instead of two registers held through the traversal)
+  [[maybe_unused]] uint32_t oct = onx0 | ony0 << 8 | onz0 << 16;
   [[maybe_unused]] float cnx = 0.f, cny = 0.f, cnz = 0.f, cfx = 0.f, cfy = 0.f, cfz = 0.f;
   if constexpr (kFma) {
     auto cpair = [](float oa, float ia, float wa, float& cn, float& cf) {
@@ -1095,6 +1102,13 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
       return tn <= tf ? ((__float_as_uint(tn) & ~3u) | c) : 0xFFFFFFFFu;
     };
     if constexpr (kOct) {
+      uint32_t onx = onx0, ony = ony0, onz = onz0;
+      if constexpr (RT_WIDE_OCTPACK) {
+        asm volatile("" : "+v"(oct));  // not loop-invariant to the compiler: unpacked here, per visit
+        onx = oct & 0xFFu;
+        ony = (oct >> 8) & 0xFFu;
+        onz = oct >> 16;
+      }
       const float4 nx = *(const float4*)(nbase + (nof + onx)), ny = *(const float4*)(nbase + (nof + ony)),
                    nz = *(const float4*)(nbase + (nof + onz));
       const float4 fx = *(const float4*)(nbase + (nof + (48u - onx))), fy = *(const float4*)(nbase + (nof + (80u - ony))),
