@@ -33,6 +33,9 @@ namespace rtd {
 #ifndef RT_WIDE_PREFETCH  // a triangle's words loaded with the record's first word (C4 358.9 -> 357.2 ms)
 #define RT_WIDE_PREFETCH 1
 #endif
+#ifndef RT_LIN_F64_RCP  // fp64 linear programs: aligned quads by the ray's refined reciprocals (round 4)
+#define RT_LIN_F64_RCP 1
+#endif
 #ifndef RT_WIDE_OCTPACK
 #define RT_WIDE_OCTPACK 1
 #endif
@@ -655,6 +658,14 @@ __device__ __forceinline__ V<R> rcp3(V<R> d) {
 #endif
   return d;
 }
+// 1/d for the flat program: v_rcp_f32 in fp32 (as rcp3), the refined reciprocal (frcp) in fp64
+template <class R>
+__device__ __forceinline__ V<R> flat_inv(V<R> d) {
+  if constexpr (sizeof(R) == 4)
+    return rcp3(d);
+  else
+    return mkv(frcp(d.x), frcp(d.y), frcp(d.z));
+}
 
 // Axis-aligned quad (rt_scene.h LinRec): n = +-e_A exactly, so quad.h:32-33 reduce to
 // t = (q_A - o_A) / d_A bit for bit; alpha = (p_U - q_U) / u_U, beta = (p_V - q_V) / v_V.
@@ -670,9 +681,15 @@ __device__ __forceinline__ R comp(V<R> v) {
 // alpha = (p - lo) * inv is -0.0 on the quad's Q edge when inv < 0 (a negative edge vector, as
 // box() faces have), which the reference accepts (0 <= -0.0) and the bit order would not: the
 // product is formed as fma(p - lo, inv, +0.0), equal to it except that -0.0 becomes +0.0.
-template <int A, int U, int W, class R>
+// RINV (fp64): inv holds the ray's refined reciprocals (flat_inv), and t is (plane - o_A) * inv_A as in the
+// flat program (within an ulp of the division) instead of a refined division per quad
+template <int A, int U, int W, class R, bool RINV = false>
 __device__ __forceinline__ bool aquad_t(const R* f, V<R> o, V<R> d, V<R> inv, R tmin, R tmax, R& t) {
-  R th = fdiv_inv(f[0] - comp<A>(o), comp<A>(d), comp<A>(inv));
+  R th;
+  if constexpr (sizeof(R) == 8 && RINV)
+    th = (f[0] - comp<A>(o)) * comp<A>(inv);
+  else
+    th = fdiv_inv(f[0] - comp<A>(o), comp<A>(d), comp<A>(inv));
   if constexpr (sizeof(R) == 4) {
     const R a = __builtin_fmaf((comp<U>(o) + th * comp<U>(d)) - f[1], f[3], 0.0f);
     const R b = __builtin_fmaf((comp<W>(o) + th * comp<W>(d)) - f[2], f[4], 0.0f);
@@ -694,13 +711,14 @@ __device__ __forceinline__ bool aquad_t(const R* f, V<R> o, V<R> d, V<R> inv, R 
 }
 template <class R>
 __device__ __forceinline__ bool lin_quad_t(const LinRec<R>& r, V<R> o, V<R> d, V<R> inv, R tmin, R tmax, R& t) {
+  constexpr bool RI = RT_LIN_F64_RCP != 0;
   switch (r.aux) {
-    case 1: return aquad_t<2, 0, 1>(r.f, o, d, inv, tmin, tmax, t);
-    case 2: return aquad_t<1, 0, 2>(r.f, o, d, inv, tmin, tmax, t);
-    case 3: return aquad_t<2, 1, 0>(r.f, o, d, inv, tmin, tmax, t);
-    case 4: return aquad_t<0, 1, 2>(r.f, o, d, inv, tmin, tmax, t);
-    case 5: return aquad_t<1, 2, 0>(r.f, o, d, inv, tmin, tmax, t);
-    case 6: return aquad_t<0, 2, 1>(r.f, o, d, inv, tmin, tmax, t);
+    case 1: return aquad_t<2, 0, 1, R, RI>(r.f, o, d, inv, tmin, tmax, t);
+    case 2: return aquad_t<1, 0, 2, R, RI>(r.f, o, d, inv, tmin, tmax, t);
+    case 3: return aquad_t<2, 1, 0, R, RI>(r.f, o, d, inv, tmin, tmax, t);
+    case 4: return aquad_t<0, 1, 2, R, RI>(r.f, o, d, inv, tmin, tmax, t);
+    case 5: return aquad_t<1, 2, 0, R, RI>(r.f, o, d, inv, tmin, tmax, t);
+    case 6: return aquad_t<0, 2, 1, R, RI>(r.f, o, d, inv, tmin, tmax, t);
     default: break;
   }
   // general quad: the fields of Quad<R> (quad.h:30-52)
@@ -1348,7 +1366,8 @@ __device__ __forceinline__ void trace_linear(const DevScene<R>& sc, V<R> wo, V<R
   const R tmin = R(0.001);
   R tmax = Num<R>::inf();
   V<R> o = wo, d = wd;
-  const V<R> winv = rcp3(wd);
+  // fp32: v_rcp_f32; fp64 (RT_LIN_F64_RCP): the refined reciprocals, once per ray and instance
+  const V<R> winv = (sizeof(R) == 8 && RT_LIN_F64_RCP) ? flat_inv(wd) : rcp3(wd);
   V<R> inv = winv;
   int32_t cur = -1;
   uint32_t jv = 0;
@@ -1395,7 +1414,7 @@ __device__ __forceinline__ void trace_linear(const DevScene<R>& sc, V<R> wo, V<R
         o = op_in(x, o, true);
         d = op_in(x, d, false);
       }
-      inv = rcp3(d);
+      inv = (sizeof(R) == 8 && RT_LIN_F64_RCP) ? flat_inv(d) : rcp3(d);
     } else if (VOL && ty == E_VOLUME) {
       const Volume<R> vol = ld_uniform(sc.vols, idx);
       h = volume_t<R, true>(sc, vol, wo, wd, d, time, tmin, tmax, keys, bounce, jv, th);
@@ -1403,7 +1422,8 @@ __device__ __forceinline__ void trace_linear(const DevScene<R>& sc, V<R> wo, V<R
       cur = -1;
       o = wo;
       d = wd;
-      inv = winv;
+      // fp64: recomputed rather than kept through the loop (6 registers)
+      inv = (sizeof(R) == 8 && RT_LIN_F64_RCP) ? flat_inv(wd) : winv;
     }
     if (h) {
       tmax = th;
@@ -1425,14 +1445,6 @@ template <class R>
 struct FlatQuad2 {
   FlatQuadT<R> a, b;
 };
-// 1/d for the flat program: v_rcp_f32 in fp32 (as rcp3), IEEE division in fp64
-template <class R>
-__device__ __forceinline__ V<R> flat_inv(V<R> d) {
-  if constexpr (sizeof(R) == 4)
-    return rcp3(d);
-  else
-    return mkv(frcp(d.x), frcp(d.y), frcp(d.z));
-}
 template <int A, class R>
 __device__ __forceinline__ void flat_quad_test(const FlatQuadT<R>& r, int32_t idx, V<R> o, V<R> d, V<R> inv,
                                                R tmin, R& tmax, int32_t& best, uint64_t xkey) {

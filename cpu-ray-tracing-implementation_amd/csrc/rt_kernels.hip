@@ -879,7 +879,7 @@ struct LinearTrav {
 };
 // The flat program (quad/box scenes such as every Cornell config): rt_device.h trace_flat.
 #ifndef RT_FLAT_WAVES
-#define RT_FLAT_WAVES 7
+#define RT_FLAT_WAVES 8
 #endif
 #ifndef RT_F64_COLD_LDS  // fp64 flat program: the cold path state (item sum, pixel, keys, camera base) in LDS
 #define RT_F64_COLD_LDS 1
@@ -891,7 +891,7 @@ struct LinearTrav {
 #define RT_FLAT_NORAD 1
 #endif
 #ifndef RT_FLAT_WAVES_F64  // fp64 flat program: waves per SIMD the register budget is cut for (1: none)
-#define RT_FLAT_WAVES_F64 4
+#define RT_FLAT_WAVES_F64 5
 #endif
 template <class R, bool TLDS = false>
 struct FlatTrav {

@@ -33,10 +33,10 @@ for p in ("pmcA", "pmcB"):
         if cnt[k] == 2:
             per[names[k]].update(c)
 instr = rates["cus"] * 4 * rates["waves_per_simd"] * rates["instr_per_wave"]
-res = {"cycles_per_wave_instr": rates["ops"], "unit": rates["unit"], "counters_per_instr": {}}
+res = {"per_wave_instr": rates["ops"], "unit": rates["unit"], "counters_per_instr": {}}
 for n in names:
     c = per.get(n, {})
     res["counters_per_instr"][n] = {k: round(v / instr, 3) for k, v in sorted(c.items())}
 json.dump(res, open(out + "/valu_rates.json", "w"), indent=1)
-print(json.dumps(res["cycles_per_wave_instr"]))
+print(json.dumps({k: v["cycles"] for k, v in res["per_wave_instr"].items()}))
 PY

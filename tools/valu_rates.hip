@@ -25,7 +25,7 @@
     }                                                                                   \
   } while (0)
 
-constexpr int kIters = 256;   // loop trips
+constexpr int kIters = 2048;  // loop trips (~131k instructions per wave: launch costs vanish)
 constexpr int kPerIter = 64;  // instructions per trip (8 chains x 8)
 
 // one op on chain register r (double / uint64 pairs, float / uint32 singles)
@@ -33,7 +33,7 @@ constexpr int kPerIter = 64;  // instructions per trip (8 chains x 8)
 
 template <int K>
 __device__ __forceinline__ void body(double& a0, double& a1, double& a2, double& a3, double& a4, double& a5,
-                                     double& a6, double& a7, double b, float& f0, float& f1, float& f2, float& f3,
+                                     double& a6, double& a7, double b, double c, float fc, float& f0, float& f1, float& f2, float& f3,
                                      float& f4, float& f5, float& f6, float& f7, float fb, uint64_t& s0, uint64_t& s1,
                                      uint64_t& s2, uint64_t& s3, uint64_t& s4, uint64_t& s5, uint64_t& s6,
                                      uint64_t& s7, uint64_t m) {
@@ -48,7 +48,7 @@ __device__ __forceinline__ void body(double& a0, double& a1, double& a2, double&
       OP8(X)
 #undef X
     } else if constexpr (K == 2) {
-#define X(r) asm volatile("v_fma_f64 %0, %0, %1, %1" : "+v"(r) : "v"(b));
+#define X(r) asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(r) : "v"(b), "v"(c));
       OP8(X)
 #undef X
     } else if constexpr (K == 3) {
@@ -72,7 +72,7 @@ __device__ __forceinline__ void body(double& a0, double& a1, double& a2, double&
       X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
 #undef X
     } else if constexpr (K == 8) {
-#define X(r) asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(f##r) : "v"(fb));
+#define X(r) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(f##r) : "v"(fb), "v"(fc));
       X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
 #undef X
     } else if constexpr (K == 9) {
@@ -115,6 +115,18 @@ __device__ __forceinline__ void body(double& a0, double& a1, double& a2, double&
 #define X(r) asm volatile("v_rsq_f32 %0, %0" : "+v"(f##r));
       X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
 #undef X
+    } else if constexpr (K == 20) {
+#define X(r) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(r) : "v"(b), "v"(c));
+      OP8(X)
+#undef X
+    } else if constexpr (K == 21) {
+#define X(r) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(f##r) : "v"(fb));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 22) {
+#define X(r) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(f##r) : "v"(fb));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
     } else if constexpr (K == 19) {
 #define X(r) { uint64_t t; asm volatile("v_cmp_class_f64_e64 %0, %1, %2" : "=s"(t) : "v"(a##r), "v"(f0)); s##r ^= t; }
       X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
@@ -126,16 +138,19 @@ __device__ __forceinline__ void body(double& a0, double& a1, double& a2, double&
 template <int K>
 __global__ __launch_bounds__(256) void k_rate(double* out, unsigned long long* clk, double seed) {
   double a0 = seed + threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6,
-         a7 = a0 + 7, b = seed * 0.5;
+         a7 = a0 + 7, b = seed * 0.5, c = seed * 0.25;
   float f0 = (float)a0, f1 = (float)a1, f2 = (float)a2, f3 = (float)a3, f4 = (float)a4, f5 = (float)a5,
-        f6 = (float)a6, f7 = (float)a7, fb = (float)b;
+        f6 = (float)a6, f7 = (float)a7, fb = (float)b, fc = (float)c;
   uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0, s5 = 0, s6 = 0, s7 = 0, m = 0x5555555555555555ull;
-  const unsigned long long t0 = clock64();
+  const unsigned long long t0 = clock64(), w0 = wall_clock64();
 #pragma unroll 1
   for (int i = 0; i < kIters; i++)
-    body<K>(a0, a1, a2, a3, a4, a5, a6, a7, b, f0, f1, f2, f3, f4, f5, f6, f7, fb, s0, s1, s2, s3, s4, s5, s6, s7, m);
-  const unsigned long long t1 = clock64();
-  if ((threadIdx.x & 63) == 0) clk[blockIdx.x * 4 + (threadIdx.x >> 6)] = t1 - t0;
+    body<K>(a0, a1, a2, a3, a4, a5, a6, a7, b, c, fc, f0, f1, f2, f3, f4, f5, f6, f7, fb, s0, s1, s2, s3, s4, s5, s6, s7, m);
+  const unsigned long long t1 = clock64(), w1 = wall_clock64();
+  if ((threadIdx.x & 63) == 0) {
+    clk[2 * (blockIdx.x * 4 + (threadIdx.x >> 6))] = t1 - t0;
+    clk[2 * (blockIdx.x * 4 + (threadIdx.x >> 6)) + 1] = w1 - w0;
+  }
   out[blockIdx.x * 256 + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 + f0 + f1 + f2 + f3 + f4 + f5 + f6 +
                                         f7 + (double)(s0 ^ s1 ^ s2 ^ s3 ^ s4 ^ s5 ^ s6 ^ s7);
 }
@@ -153,7 +168,8 @@ int main() {
       {"v_cndmask_b32", k_rate<9>},    {"v_lshl_add_u64", k_rate<10>},   {"v_cmp_gt_u64", k_rate<11>},
       {"v_rcp_f64", k_rate<12>},       {"v_floor_f64", k_rate<13>},      {"v_cvt_f64_u32", k_rate<14>},
       {"v_mul_lo_u32", k_rate<15>},    {"v_ldexp_f64", k_rate<16>},      {"v_lshlrev_b64", k_rate<17>},
-      {"v_rsq_f32", k_rate<18>},       {"v_cmp_class_f64", k_rate<19>},
+      {"v_rsq_f32", k_rate<18>},       {"v_cmp_class_f64", k_rate<19>},  {"v_pk_fma_f32", k_rate<20>},
+      {"v_mul_f32", k_rate<21>},       {"v_xor_b32", k_rate<22>},
   };
   int ncu = 0;
   CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
@@ -161,24 +177,38 @@ int main() {
   double* out;
   unsigned long long* clk;
   CHECK(hipMalloc(&out, sizeof(double) * blocks * 256));
-  CHECK(hipMalloc(&clk, sizeof(unsigned long long) * blocks * 4));
-  std::vector<unsigned long long> h(blocks * 4);
+  CHECK(hipMalloc(&clk, sizeof(unsigned long long) * blocks * 8));
+  std::vector<unsigned long long> h(blocks * 8);
+  int wall_khz = 0;
+  CHECK(hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, 0));
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
   std::printf("{\"cus\": %d, \"waves_per_simd\": %d, \"instr_per_wave\": %d, \"ops\": {", ncu, waves_per_simd,
               kIters * kPerIter);
   for (size_t i = 0; i < sizeof(es) / sizeof(es[0]); i++) {
+    float ms = 0;
     for (int rep = 0; rep < 2; rep++) {  // the first launch warms up
+      CHECK(hipEventRecord(e0, 0));
       hipLaunchKernelGGL(es[i].k, dim3(blocks), dim3(256), 0, 0, out, clk, 1.25);
+      CHECK(hipEventRecord(e1, 0));
       CHECK(hipGetLastError());
       CHECK(hipDeviceSynchronize());
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
     }
     CHECK(hipMemcpy(h.data(), clk, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
-    double mean = 0;
-    for (auto c : h) mean += (double)c;
-    mean /= (double)h.size();
-    const double cpi = mean / ((double)waves_per_simd * kIters * kPerIter);
-    std::printf("%s\"%s\": %.3f", i ? ", " : "", es[i].name, cpi);
+    double c = 0, w = 0;
+    for (size_t j = 0; j < h.size(); j += 2) c += (double)h[j], w += (double)h[j + 1];
+    c /= (double)(h.size() / 2);
+    w /= (double)(h.size() / 2);
+    const double instr = (double)waves_per_simd * kIters * kPerIter;  // per SIMD
+    const double ghz = c / (w / (wall_khz * 1e3)) / 1e9;                // shader clock from clock64 / wall clock
+    // cycles per wave64 instruction per SIMD: from the shader clock inside the loop, and from the
+    // kernel's event time at that clock
+    std::printf("%s\"%s\": {\"cycles\": %.3f, \"cycles_event\": %.3f, \"ghz\": %.3f}", i ? ", " : "", es[i].name,
+                c / instr, ms * 1e-3 * ghz * 1e9 / instr, ghz);
   }
-  std::printf("}, \"unit\": \"shader-clock cycles per wave64 instruction per SIMD (8 waves/SIMD, 8 chains)\"}\n");
+  std::printf("}, \"unit\": \"shader-clock cycles per wave64 instruction per SIMD (8 waves/SIMD, 8 chains); ghz = clock64 rate against wall_clock64\", \"wall_khz\": %d}\n", wall_khz);
   CHECK(hipFree(out));
   CHECK(hipFree(clk));
   return 0;
