@@ -34,7 +34,7 @@ namespace rtd {
 #define RT_WIDE_PREFETCH 1
 #endif
 #ifndef RT_LIN_F64_RCP  // fp64 linear programs: aligned quads by the ray's refined reciprocals (round 4)
-#define RT_LIN_F64_RCP 1
+#define RT_LIN_F64_RCP 0
 #endif
 #ifndef RT_WIDE_OCTPACK
 #define RT_WIDE_OCTPACK 1

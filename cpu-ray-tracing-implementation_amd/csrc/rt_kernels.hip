@@ -80,8 +80,11 @@ constexpr int kBlock = 256;
 #define RT_STACK_WAVES_F64 4  // 4: 1,704); with the nodes in LDS (C3 fp64) none: 260 ms, 3: 295, 4: 276
 #endif
 #ifndef RT_LINEAR_VOL_WAVES  // fp32 quad + volume linear program (C5), with slab-tested box() volumes: 1 (4 waves at
-                             // 128 VGPRs) 1661 ms/frame, 5: 1567, 6: 2594 (spills)
-#define RT_LINEAR_VOL_WAVES 5
+                             // 128 VGPRs) 1661 ms/frame, 5: 1567, 6: 2594 (spills); round 4 (cold state in LDS,
+#define RT_LINEAR_VOL_WAVES 6  // radiance folded, table sin/cos): 5: 1,326, 6: 1,247
+#endif
+#ifndef RT_LINEAR_VOL_WAVES_F64  // the fp64 volume program (round 4, cold state in LDS): 3 waves 2,672 ms/frame, 4: 2,400
+#define RT_LINEAR_VOL_WAVES_F64 4
 #endif
 constexpr int kBatch = 16;           // extend/shade rounds between live-slot counts
 constexpr int kSegShards = 256;      // segment counter shards
@@ -859,7 +862,7 @@ struct LinearTrav {
   static constexpr int kStack = 0;
   // waves per SIMD the register budget is cut for (occupancy hides the shading loads); the
   // lean quad-only program fits 96 VGPRs with a small spill, the others would spill heavily
-  static constexpr int kWaves = sizeof(R) != 4 ? RT_LINEAR_WAVES_F64
+  static constexpr int kWaves = sizeof(R) != 4 ? (VOL ? RT_LINEAR_VOL_WAVES_F64 : RT_LINEAR_WAVES_F64)
                                  : (!SPH && !TRI && !VOL) ? RT_LINEAR_WAVES
                                  : (!SPH && !TRI && VOL)  ? RT_LINEAR_VOL_WAVES
                                                           : 1;

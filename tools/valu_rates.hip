@@ -127,6 +127,78 @@ __device__ __forceinline__ void body(double& a0, double& a1, double& a2, double&
 #define X(r) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(f##r) : "v"(fb));
       X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
 #undef X
+    } else if constexpr (K == 23) {
+#define X(r) asm volatile("v_mov_b32 %0, %1" : "=v"(f##r) : "v"(f##r));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 24) {
+#define X(r) asm volatile("s_mov_b64 vcc, %2\n\tv_cndmask_b32 %0, %0, %1, vcc" : "+v"(f##r) : "v"(fb), "s"(m) : "vcc");
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 25) {
+#define X(r) { uint64_t t; asm volatile("v_cmp_lt_f32_e64 %0, %1, %2" : "=s"(t) : "v"(f##r), "v"(fb)); s##r ^= t; }
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 26) {
+#define X(r) asm volatile("v_add_u32 %0, %0, %1" : "+v"(f##r) : "v"(fb));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 27) {
+#define X(r) asm volatile("v_lshrrev_b32 %0, 1, %0" : "+v"(f##r));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 28) {
+#define X(r) asm volatile("v_bfe_u32 %0, %0, 3, 7" : "+v"(f##r));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 29) {
+#define X(r) { uint64_t t; asm volatile("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(a##r), "=s"(t) : "v"(f##r), "v"(fb), "v"(a##r)); s##r ^= t; }
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 30) {
+#define X(r) asm volatile("v_min_f32 %0, %0, %1" : "+v"(f##r) : "v"(fb));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 31) {
+#define X(r) { uint32_t t; asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(t) : "v"(f##r)); s##r ^= t; }
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 32) {
+#define X(r) asm volatile("v_fract_f64 %0, %0" : "+v"(a##r));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 33) {
+#define X(r) asm volatile("v_rsq_f64 %0, %0" : "+v"(a##r));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 34) {
+#define X(r) asm volatile("v_sqrt_f32 %0, %0" : "+v"(f##r));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 35) {
+#define X(r) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(f##r) : "v"(fb));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 36) {
+#define X(r) asm volatile("v_cvt_f32_u32 %0, %0" : "+v"(f##r));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 37) {
+#define X(r) asm volatile("v_min_f64 %0, %0, %1" : "+v"(a##r) : "v"(b));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 38) {
+#define X(r) { uint64_t t; asm volatile("v_cmp_eq_u32_e64 %0, %1, %2" : "=s"(t) : "v"(f##r), "v"(fb)); s##r ^= t; }
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 39) {
+#define X(r) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x78" : "+v"(f##r) : "v"(fb), "v"(fc));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 40) {
+#define X(r) { asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(f##r) : "v"(fb), "s"(m)); }
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
     } else if constexpr (K == 19) {
 #define X(r) { uint64_t t; asm volatile("v_cmp_class_f64_e64 %0, %1, %2" : "=s"(t) : "v"(a##r), "v"(f0)); s##r ^= t; }
       X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
@@ -170,6 +242,7 @@ int main() {
       {"v_mul_lo_u32", k_rate<15>},    {"v_ldexp_f64", k_rate<16>},      {"v_lshlrev_b64", k_rate<17>},
       {"v_rsq_f32", k_rate<18>},       {"v_cmp_class_f64", k_rate<19>},  {"v_pk_fma_f32", k_rate<20>},
       {"v_mul_f32", k_rate<21>},       {"v_xor_b32", k_rate<22>},
+      {"v_mov_b32", k_rate<23>}, {"v_cndmask_b32_vcc", k_rate<24>}, {"v_cmp_lt_f32", k_rate<25>}, {"v_add_u32", k_rate<26>}, {"v_lshrrev_b32", k_rate<27>}, {"v_bfe_u32", k_rate<28>}, {"v_mad_u64_u32", k_rate<29>}, {"v_min_f32", k_rate<30>}, {"v_readfirstlane_b32", k_rate<31>}, {"v_fract_f64", k_rate<32>}, {"v_rsq_f64", k_rate<33>}, {"v_sqrt_f32", k_rate<34>}, {"v_mul_hi_u32", k_rate<35>}, {"v_cvt_f32_u32", k_rate<36>}, {"v_min_f64", k_rate<37>}, {"v_cmp_eq_u32", k_rate<38>}, {"v_bitop3_b32", k_rate<39>}, {"v_cndmask_b32_e64_v", k_rate<40>}, 
   };
   int ncu = 0;
   CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
