@@ -29,18 +29,77 @@ from rt_amd import abi, buildinfo, plugin  # noqa: E402
 from rt_amd.distributed import FrameSharding  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
-# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD every 2 cycles at the
-# 2.4 GHz max clock (MI355X_MICROARCH.md, "Wave scheduling")
-SIMDS, CLOCK_GHZ, VALU_CYCLES = 1024, 2.4, 2
-VALU_PEAK_G = SIMDS * CLOCK_GHZ / VALU_CYCLES  # G wave-instructions/s
-# fp64 issues at half the fp32 vector rate (MI355X spec: 78.6 vs 157.3 TFLOPS vector): a wave64 fp64
-# add / mul / fma / transcendental holds its SIMD 4 cycles, any other VALU instruction 2. The fp64 line's
-# roofline is therefore in SIMD cycles, from the rocprofv3 instruction-mix counters (SQ_INSTS_VALU_*_F64):
-# SQ_ACTIVE_INST_VALU counts one unit per instruction whatever its width (r03a: 59.6 G against 52.9 G
-# instructions on the fp64 kernel, 1.03x on the fp32 one), so it cannot weight fp64 by its issue time.
-F64_CYCLES = 4
-CYCLE_PEAK_G = SIMDS * CLOCK_GHZ  # G SIMD-cycles/s
-F64_MIX = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64")
+SIMDS, CLOCK_GHZ = 1024, 2.4  # 256 CUs x 4 SIMDs; the 2.4 GHz peak engine clock (MI355X_MICROARCH.md)
+CYCLE_PEAK_G = SIMDS * CLOCK_GHZ  # G SIMD-cycles/s: every SIMD issuing VALU work every cycle
+# VALU roofline: SIMD cycles per launch = sum over the kernel's VALU instructions of the cycles
+# each holds its SIMD, measured on this MI355X for single opcodes (tools/valu_rates.hip, 8 waves/SIMD, 8
+# independent chains; kernel time x the measured shader clock: profiles/r04c_valu_rates.json) and rounded to
+# the issue cost they show: 2 cycles per wave64 instruction for 32-bit add/mul/fma/logic/moves (measured
+# 2.2-2.4), 4 for every fp64 operation (add/mul/fma/min/max/floor/fract/ldexp), 64-bit moves and shifts,
+# conversions, bit-field extracts, 32-bit integer multiplies, fp32 min/max and v_cndmask with an SGPR mask
+# (4.1-4.3), 4.6 for compares into an SGPR mask (VOPC, any width: 4.7-4.9), 4.8 for v_mad_u64_u32 (5.0),
+# 5.7 for v_readfirstlane (5.9), 8 for fp32 transcendentals (8.1) and 16 for fp64 ones (v_rcp_f64 /
+# v_rsq_f64: 16.2).
+VALU_PMC_CLASSES = {  # SQ_INSTS_VALU_* class counters -> the static-mix class they count
+    "f64_addmulfma": ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64"),
+    "f64_trans": ("SQ_INSTS_VALU_TRANS_F64",),
+    "f32_trans": ("SQ_INSTS_VALU_TRANS_F32",),
+    "cvt": ("SQ_INSTS_VALU_CVT",),
+    "int64": ("SQ_INSTS_VALU_INT64",),
+}
+
+
+def opcode_cycles(op):
+    """Issue cycles of one wave64 VALU opcode on gfx950 (the table above)."""
+    import re
+    if re.match(r"v_(rcp|rsq|sqrt|exp|log|sin|cos)_f64", op):
+        return 16.0
+    if re.match(r"v_(rcp|rsq|sqrt|exp|log|sin|cos|rcp_iflag)_f32", op):
+        return 8.0
+    if op.startswith("v_cmp"):
+        return 4.6
+    if op.startswith(("v_mad_u64_u32", "v_mad_i64_i32")):
+        return 4.8
+    if op.startswith(("v_readfirstlane", "v_readlane", "v_writelane")):
+        return 5.7
+    if ("f64" in op or "_b64" in op or "_u64" in op or "_i64" in op or op.startswith(("v_cvt", "v_bfe", "v_pk_"))
+            or re.match(r"v_mul_(lo|hi)_", op) or re.match(r"v_(min|max|med3)_f32", op)
+            or op.startswith("v_cndmask_b32_e64")):
+        return 4.0
+    return 2.0
+
+
+def issue_cycles(counters, mix):
+    """SIMD cycles per launch: the classes the SQ_INSTS_VALU_* counters count, each at the mean cost of its
+    opcodes in the kernel's static mix (scripts/valu_static_mix.py), and the remaining VALU instructions at
+    the mean cost of the remaining opcodes -- fp64 compares, min/max and the like included. Returns
+    (cycles, {class: (instructions, cycles per instruction)})."""
+    import sys as _s
+    _s.path.insert(0, os.path.join(REPO, "scripts"))
+    from valu_static_mix import classify
+    ops = mix["opcodes"]
+    by_class = {}
+    for op, n in ops.items():
+        by_class.setdefault(classify(op), []).append((op, n))
+
+    def mean_cost(items, default):
+        tot = sum(n for _, n in items)
+        return sum(opcode_cycles(op) * n for op, n in items) / tot if tot else default
+    parts, counted = {}, 0.0
+    for cl, names in VALU_PMC_CLASSES.items():
+        if all(k in counters for k in names):
+            n = sum(counters[k] for k in names)
+            parts[cl] = (n, mean_cost(by_class.get(cl, []), opcode_cycles({"f64_addmulfma": "v_add_f64",
+                                                                           "f64_trans": "v_rcp_f64",
+                                                                           "f32_trans": "v_rcp_f32",
+                                                                           "cvt": "v_cvt_f32_f64",
+                                                                           "int64": "v_lshl_add_u64"}[cl])))
+            counted += n
+    rest_items = [(op, n) for cl, items in by_class.items() if cl not in parts for op, n in items]
+    parts["rest"] = (max(0.0, counters["SQ_INSTS_VALU"] - counted), mean_cost(rest_items, 2.0))
+    return sum(n * c for n, c in parts.values()), parts
+
+
 # SURVEY.md §8(d) algorithmic bytes: per sample (generate + finalise) and per segment
 B_GEN, B_ACC, B_EXT, B_SHADE = 64, 36, 44, 152
 
@@ -214,11 +273,10 @@ def roofline(key, st, segs, my_samples, elapsed, kern, fp64):
     alg_bytes = (B_GEN + B_ACC) * my_samples + (B_EXT + B_SHADE) * segs
     avg_s = step_ms / 1e3 / iters
     mp = measured_pmc(key)
-    roof = {"bound": "valu", "kernel": kern, "unit": "G VALU wave-instr/s", "peak": VALU_PEAK_G,
+    roof = {"bound": "valu", "kernel": kern, "unit": "G SIMD-cycles/s", "peak": CYCLE_PEAK_G,
             "achieved": None, "frac": None, "traffic": None,
             "avg_launch_us": round(avg_s * 1e6, 2), "launches": iters,
             "kernel_share_of_wall": round(step_ms / 1e3 / elapsed, 4),
-            "peak_basis": "1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction",
             "wavefront_equiv": {"alg_bytes_per_launch": int(alg_bytes / iters),
                                 "GBps": round(alg_bytes / (step_ms / 1e3) / 1e9, 1),
                                 "note": "SURVEY §8(d) bytes a classic SoA wavefront would move for "
@@ -226,23 +284,34 @@ def roofline(key, st, segs, my_samples, elapsed, kern, fp64):
     if not mp:
         return roof
     d = mp[1]
-    c = d.get("counters", {})
-    achieved = d["valu_per_launch"] / avg_s / 1e9
-    roof.update({"achieved": round(achieved, 2), "frac": round(achieved / VALU_PEAK_G, 4),
-                 "valu_per_launch": d["valu_per_launch"], "pmc_source": "profiles/" + mp[0],
-                 "frac_at_measured_clock": d.get("valu_issue_frac_measured_clock"),
+    c = dict(d.get("counters", {}))
+    c["SQ_INSTS_VALU"] = d["valu_per_launch"]
+    mix = None
+    if d.get("valu_mix"):
+        with open(os.path.join(REPO, "profiles", d["valu_mix"])) as fh:
+            mix = json.load(fh)
+    roof.update({"valu_per_launch": d["valu_per_launch"], "pmc_source": "profiles/" + mp[0],
                  "lane_valu_per_segment": round(d["valu_per_launch"] * 64 / (segs / iters), 1),
                  "valu_lane_util": d.get("valu_lane_util"), "wait_frac": d.get("wait_frac")})
-    if fp64 and all(k in c for k in F64_MIX):
-        # issue time weighted by width: fp64 instructions hold the SIMD twice as long
-        n64 = sum(c[k] for k in F64_MIX)
-        cycles = VALU_CYCLES * (d["valu_per_launch"] - n64) + F64_CYCLES * n64
-        ach = cycles / avg_s / 1e9
-        roof.update({"unit": "G SIMD-cycles/s", "peak": CYCLE_PEAK_G, "achieved": round(ach, 2),
-                     "frac": round(ach / CYCLE_PEAK_G, 4), "frac_unweighted": round(achieved / VALU_PEAK_G, 4),
-                     "fp64_instr_per_launch": n64, "valu_cycles_per_launch": cycles,
-                     "peak_basis": "1024 SIMDs x 2.4 GHz; VALU cycles = 2 per wave64 instruction, 4 per fp64 "
-                                   "add/mul/fma/transcendental (SQ_INSTS_VALU_*_F64; fp64 vector rate = 1/2 fp32)"})
+    if mix is None:  # no static mix of this build: instructions at 2 cycles, the counted fp64 ones at 4
+        n64 = sum(c.get(k, 0.0) for k in VALU_PMC_CLASSES["f64_addmulfma"] + VALU_PMC_CLASSES["f64_trans"])
+        cycles, parts = 2.0 * (d["valu_per_launch"] - n64) + 4.0 * n64, None
+    else:
+        cycles, parts = issue_cycles(c, mix)
+    ach = cycles / avg_s / 1e9
+    gui = d.get("grbm_gui_active_per_launch")
+    roof.update({"unit": "G SIMD-cycles/s", "peak": CYCLE_PEAK_G, "achieved": round(ach, 2),
+                 "frac": round(ach / CYCLE_PEAK_G, 4), "valu_cycles_per_launch": cycles,
+                 # the same cycles against the clock the GPU actually ran during the profiled launches
+                 "frac_at_measured_clock": round(cycles / (SIMDS * gui / 8), 4) if gui else None,
+                 "cycles_by_class": ({k: {"instr": round(n), "cycles_per_instr": round(cc, 3)} for k, (n, cc) in
+                                      parts.items()} if parts else None),
+                 "valu_mix": ("profiles/" + d["valu_mix"]) if d.get("valu_mix") else None,
+                 "peak_basis": "1024 SIMDs x 2.4 GHz; SIMD cycles per VALU opcode measured (tools/valu_rates.hip, "
+                               "profiles/r04c_valu_rates.json): 2 for 32-bit add/mul/fma/logic, 4 for fp64 and "
+                               "64-bit ops, conversions, SGPR-mask selects, 4.6 compares, 8 / 16 fp32 / fp64 "
+                               "transcendentals; per-class counts from SQ_INSTS_VALU_* counters, the rest at "
+                               "the kernel's static opcode mix"})
     if roof["valu_lane_util"] is not None:  # issued lanes that do work: idle lanes of a divergent wave do not
         roof["useful_frac"] = round(roof["frac"] * roof["valu_lane_util"], 4)
     if d.get("hbm_bytes_per_launch") is not None:

@@ -77,6 +77,21 @@ def main():
         return (sum(v) / len(v), len(v)) if v else (None, 0)
     valu, nv = fam_mean("SQ_INSTS_VALU")
     gui, _ = fam_mean("GRBM_GUI_ACTIVE")
+    # the dominant kernel instantiation (longest total time in the kernel trace) and its static VALU opcode
+    # mix (scripts/valu_static_mix.py), for bench.py's issue-cycle model
+    mix_file = None
+    if stats:
+        with open(stats[0]) as fh:
+            top = max(csv.DictReader(fh), key=lambda r: float(r["TotalDurationNs"]))
+        kname = top["Name"][5:] if top["Name"].startswith("void ") else top["Name"]
+        kname = kname.split("((anonymous namespace)::Params")[0]
+        sys.path.insert(0, os.path.join(REPO, "scripts"))
+        import subprocess
+        lib = os.environ.get("RT_HIP_LIB") or os.path.join(REPO, "cpu-ray-tracing-implementation_amd", "build",
+                                                          "librt_hip.so")
+        mix_file = f"{tag}_valu_mix.json"
+        subprocess.run([sys.executable, os.path.join(REPO, "scripts", "valu_static_mix.py"), lib, kname, "--out",
+                        os.path.join(out, mix_file)], check=True)
     if valu is not None:
         sys.path.insert(0, os.path.join(REPO, "cpu-ray-tracing-implementation_amd", "python"))
         from rt_amd import buildinfo
@@ -90,6 +105,7 @@ def main():
              "wait_frac": (round(fam_mean("SQ_WAIT_ANY")[0] / fam_mean("SQ_WAVE_CYCLES")[0], 4)
                            if fam_mean("SQ_WAIT_ANY")[0] and fam_mean("SQ_WAVE_CYCLES")[0] else None),
              "hbm_bytes_per_launch": traffic["bytes_per_launch"] if fetch and write else None,
+             "valu_mix": mix_file,
              "counters": {c: fam_mean(c)[0] for c in sorted({c for k, cs in acc.items() if k.startswith(fam)
                                                              for c in cs})},
              "formulas": {"valu_issue_frac_measured_clock": "SQ_INSTS_VALU * 2 / (1024 SIMDs * GRBM_GUI_ACTIVE / 8 "
