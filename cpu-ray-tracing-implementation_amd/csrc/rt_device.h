@@ -33,6 +33,12 @@ namespace rtd {
 #ifndef RT_WIDE_PREFETCH  // a triangle's words loaded with the record's first word (C4 358.9 -> 357.2 ms)
 #define RT_WIDE_PREFETCH 1
 #endif
+#ifndef RT_FLAT_BOX_EXCL_F64  // fp64 flat boxes exclude the face the ray leaves (1) or rely on tmin (0, flat_slab)
+#define RT_FLAT_BOX_EXCL_F64 1
+#endif
+#ifndef RT_LIGHT_PDF_F64  // fp64 axis-aligned light pdf by one reciprocal (light_pdf_aligned, round 4)
+#define RT_LIGHT_PDF_F64 1
+#endif
 #ifndef RT_LIN_F64_RCP  // fp64 linear programs: aligned quads by the ray's refined reciprocals (round 4)
 #define RT_LIN_F64_RCP 0
 #endif
@@ -98,6 +104,29 @@ __device__ __forceinline__ double frsq(double x) {  // 1/sqrt(x)
   r = r * fma(-h * r, r, 1.5);
   return __builtin_isfinite(r) ? r : r0;
 }
+// 1/sqrt(x) without the fallback (round 4): for unit(v), where it cannot matter -- a zero vector gives NaN
+// with or without it (0 * inf), as the reference's v / 0 does -- and the class test and two selects it
+// costs are 13 of the ~30 SIMD cycles of the refined rsqrt (measured issue costs)
+__device__ __forceinline__ double frsq_nz(double x) {
+  const double r0 = __builtin_amdgcn_rsq(x);
+  const double h = 0.5 * x;
+  double r = r0;
+  r = r * fma(-h * r, r, 1.5);
+  r = r * fma(-h * r, r, 1.5);
+  return r;
+}
+// sqrt of x in [0, 1] (the sampling formulas' sqrt(r2), sqrt(1 - r2), sqrt(1 - cos^2)): x = 0 is the only
+// operand the refinement cannot take (rsq(0) = inf), so one compare replaces fsqrt's three
+__device__ __forceinline__ double fsqrt01(double x) {
+  const double r = __builtin_amdgcn_rsq(x);
+  double g = x * r, h = 0.5 * r;
+  const double e = fma(-g, h, 0.5);
+  g = fma(g, e, g);
+  h = fma(h, e, h);
+  g = fma(fma(-g, g, x), h, g);
+  return x > 0.0 ? g : 0.0;
+}
+__device__ __forceinline__ float fsqrt01(float x) { return fsqrt(x); }
 __device__ __forceinline__ double fsqrt(double x) {
   const double r = __builtin_amdgcn_rsq(x);
   double g = x * r, h = 0.5 * r;
@@ -236,7 +265,7 @@ __device__ __forceinline__ V<float> unit(V<float> a) {  // vec3.h:77 (v / |v|), 
 }
 template <>
 __device__ __forceinline__ V<double> unit(V<double> a) {  // vec3.h:77 (v / |v|), as v * rsqrt(v.v) refined
-  return a * frsq(a.x * a.x + a.y * a.y + a.z * a.z);
+  return a * frsq_nz(a.x * a.x + a.y * a.y + a.z * a.z);
 }
 
 template <class R>
@@ -1491,11 +1520,15 @@ template <class R>
 struct Slab {
   R t0[3], t1[3], tn, tf, th;
 };
+// RT_FLAT_BOX_EXCL_F64 = 0 (fp64): no face exclusion. The face a ray leaves is at distance |t| ~ ulp(o) / |d_k|
+// from it, below tmin = 0.001 unless the ray grazes the face, which is also when the reference's own quad
+// test of that face (quad.h:30-35, no exclusion either) re-hits it; the six selects per box cost ~100 SIMD
+// cycles per segment.
 template <class R>
 __device__ __forceinline__ Slab<R> flat_slab(const FlatBoxT<R>& b, V<R> o, V<R> inv, R tmin, int32_t excl_i,
                                              uint32_t xf) {
   Slab<R> s;
-  const bool left = excl_i == b.inst;
+  const bool left = (sizeof(R) == 4 || RT_FLAT_BOX_EXCL_F64) && excl_i == b.inst;
   const R ninf = -Num<R>::inf();
   s.t0[0] = (left & (xf == 0)) ? ninf : (b.lo[0] - o.x) * inv.x;
   s.t1[0] = (left & (xf == 1)) ? ninf : (b.hi[0] - o.x) * inv.x;
@@ -1749,7 +1782,7 @@ __device__ __forceinline__ V<R> onb_transform(const Onb<R>& b, V<R> v) {  // onb
 template <class R>
 __device__ __forceinline__ V<R> on_sphere(R u1, R u2) {
   R cos_theta = R(1) - R(2) * u1;
-  R sin_theta = fsqrt(R(1) - cos_theta * cos_theta);
+  R sin_theta = fsqrt01(R(1) - cos_theta * cos_theta);
   R sp, cp;
   sincos2pi(u2, sp, cp);
   return mkv(sin_theta * cp, cos_theta, sin_theta * sp);
@@ -1759,8 +1792,8 @@ template <class R>
 __device__ __forceinline__ V<R> cosine_dir(R r1, R r2) {
   R sp, cp;
   sincos2pi(r1, sp, cp);
-  R sr2 = fsqrt(r2);
-  return mkv(cp * sr2, fsqrt(R(1) - r2), sp * sr2);
+  R sr2 = fsqrt01(r2);
+  return mkv(cp * sr2, fsqrt01(R(1) - r2), sp * sr2);
 }
 
 // hittable_pdf over the light (hittable_list.h:39-50 -> quad.h:66-78 / sphere.h:76-81 / hittable.h:39-41)
@@ -1782,6 +1815,22 @@ template <class R>
 struct LightAF {  // Light::af
   R f[8];
 };
+// quad::pdf_value of an axis-aligned light in fp64 (round 4): one refined reciprocal of d_A serves the hit
+// distance t = (q_A - o_A) / d_A and the cosine |d_A| / |d|, so distance_squared / (cosine * area) =
+// t^2 (d.d) |d| |1/d_A| / area, |d| = (d.d) rsqrt(d.d) (the rsqrt unit(dir) computes too), 1/area stored
+// (af[7]): one reciprocal instead of two refined divisions and no dot product with the normal (+-e_A).
+// Within a few ulp of the reference's expression; the hit test is aquad_t's.
+template <int A, int U, int W>
+__device__ __forceinline__ double light_pdf_aligned(const double* f, V<double> o, V<double> d) {
+  const double rA = frcp(comp<A>(d));
+  const double th = (f[0] - comp<A>(o)) * rA;
+  if (!(0.001 <= th)) return 0.0;  // interval(0.001, inf) (quad.h:70); th = +inf fails the alpha test
+  const double a = ((comp<U>(o) + th * comp<U>(d)) - f[1]) * f[3];
+  const double b = ((comp<W>(o) + th * comp<W>(d)) - f[2]) * f[4];
+  if (!(0.0 <= a && a <= 1.0 && 0.0 <= b && b <= 1.0)) return 0.0;
+  const double dd = d.x * d.x + d.y * d.y + d.z * d.z;
+  return ((th * th) * dd) * (dd * frsq_nz(dd)) * fabs(rA) * f[7];
+}
 template <class R>
 __device__ __forceinline__ R light_pdf(const Light<R>* Lp, V<R> o, V<R> dir, bool sampled = false) {
   const int32_t kind = ld_here(&Lp->kind);
@@ -1789,6 +1838,19 @@ __device__ __forceinline__ R light_pdf(const Light<R>* Lp, V<R> o, V<R> dir, boo
     R t;
     bool hit;
     const int32_t aligned = ld_here(&Lp->aligned);
+    if constexpr (sizeof(R) == 8 && RT_LIGHT_PDF_F64) {
+      if (aligned) {  // uniform branch
+        const LightAF<R> af = ld_here(reinterpret_cast<const LightAF<R>*>(Lp->af));
+        switch (aligned) {
+          case 1: return light_pdf_aligned<2, 0, 1>(af.f, o, dir);
+          case 2: return light_pdf_aligned<1, 0, 2>(af.f, o, dir);
+          case 3: return light_pdf_aligned<2, 1, 0>(af.f, o, dir);
+          case 4: return light_pdf_aligned<0, 1, 2>(af.f, o, dir);
+          case 5: return light_pdf_aligned<1, 2, 0>(af.f, o, dir);
+          default: return light_pdf_aligned<0, 2, 1>(af.f, o, dir);
+        }
+      }
+    }
     if (sizeof(R) == 4 && sampled) {
       t = R(1);
       hit = true;

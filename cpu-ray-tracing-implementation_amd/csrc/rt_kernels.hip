@@ -977,7 +977,7 @@ struct StackTrav {
 #define RT_PARAM_RELOAD 1
 #endif
 #ifndef RT_WIDE_RELOAD
-#define RT_WIDE_RELOAD 0
+#define RT_WIDE_RELOAD 1  // round 4 (lean state): C3 fp32 51.9 -> 51.1 ms/frame, fp64 71.3 -> 70.7, C4 neutral
 #endif
 #ifndef RT_SHADE_BATCH  // < 64: a wave stops traversing to shade once this many of its lanes have finished
 #define RT_SHADE_BATCH 48  // (LDS-resident tree, C3 fp32 ms/frame: never 57.06, 48: 52.57, 52: 52.58, 56: 52.81, 60: 53.57; fp64 81.3 -> 75.8)

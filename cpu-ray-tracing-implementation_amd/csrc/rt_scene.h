@@ -256,7 +256,7 @@ struct alignas(16) Light {
   R pad2;
   R center[3];  // L_SPHERE: center_ (sphere.h:76-81)
   R radius;
-  R af[8];  // aligned L_QUAD: q[A], q[U], q[V], 1/u[U], 1/v[V], u[U], v[V]
+  R af[8];  // aligned L_QUAD: q[A], q[U], q[V], 1/u[U], 1/v[V], u[U], v[V], 1/area
 };
 
 // What the host uploads: offsets into one contiguous device blob.

@@ -593,6 +593,7 @@ void Compiler::light_from(int idx) {
       light_.af[4] = 1.0 / qv_.back();
       light_.af[5] = qu_.back();
       light_.af[6] = qv_.back();
+      light_.af[7] = 1.0 / light_.quad.area;  // fp64 light_pdf_aligned
     }
     quads_.resize(before);
     aligned_.resize(before);
