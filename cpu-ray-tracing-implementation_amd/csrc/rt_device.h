@@ -34,7 +34,7 @@ namespace rtd {
 #define RT_WIDE_PREFETCH 1
 #endif
 #ifndef RT_FLAT_BOX_EXCL_F64  // fp64 flat boxes exclude the face the ray leaves (1) or rely on tmin (0, flat_slab)
-#define RT_FLAT_BOX_EXCL_F64 1
+#define RT_FLAT_BOX_EXCL_F64 0  // C2 fp64 34.6 -> 32.7 ms/frame; full-size C1 / C2 parity unchanged (r04e)
 #endif
 #ifndef RT_LIGHT_PDF_F64  // fp64 axis-aligned light pdf by one reciprocal (light_pdf_aligned, round 4)
 #define RT_LIGHT_PDF_F64 1
