@@ -5,8 +5,13 @@ BUILD    := $(PKG)/build
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 # -ffp-contract=on: contraction decided per source expression, so the persistent and the
-# launch-per-K kernels (same shade code, different inlining) produce bit-identical images
-HIPFLAGS ?= -O3 -std=c++17 -fPIC -Wall -ffp-contract=on --offload-arch=$(ARCH)
+# launch-per-K kernels (same shade code, different inlining) produce bit-identical images.
+# -fno-slp-vectorize: the SLP vectoriser paired fp32 values into packed-math operands ((x, -x) pairs
+# for v_pk_mul_f32 / v_pk_fma_f32), which hold two registers and issue in 4 cycles for 2 lanes' worth --
+# no faster than two plain fp32 ops on gfx950 (tools/valu_rates) -- and those pairs were what spilled:
+# off, the fp32 wide and volume kernels have no scratch, and C2 fp32 21.2 -> 20.4 ms/frame, C3 fp32
+# 51.0 -> 49.7, C5 fp32 1,249 -> 1,179 (r04f)
+HIPFLAGS ?= -O3 -std=c++17 -fPIC -Wall -ffp-contract=on -fno-slp-vectorize --offload-arch=$(ARCH)
 
 LIB_SRCS := $(PKG)/csrc/rt_kernels.hip $(PKG)/csrc/rt_multi.hip $(PKG)/csrc/scene_compile.cpp
 LIB_HDRS := $(PKG)/csrc/rt_device.h $(PKG)/csrc/rt_sin.h $(PKG)/csrc/rt_scene.h $(PKG)/csrc/scene_compile.h include/rt_hip.h

@@ -312,8 +312,25 @@ def roofline(key, st, segs, my_samples, elapsed, kern, fp64):
                                "64-bit ops, conversions, SGPR-mask selects, 4.6 compares, 8 / 16 fp32 / fp64 "
                                "transcendentals; per-class counts from SQ_INSTS_VALU_* counters, the rest at "
                                "the kernel's static opcode mix"})
+    if d.get("tcp_accesses_per_launch"):
+        # the L1 / texture-address path: the TA units process about one cache access per clock per CU, and
+        # a kernel whose node and primitive fetches keep them busy every cycle (C4's tree in HBM) is bound
+        # there, whatever its VALU fraction: then that is the roofline reported
+        acc = d["tcp_accesses_per_launch"]
+        ta = {"achieved": round(acc / avg_s / 1e9, 2), "peak": round(256 * CLOCK_GHZ, 1),
+              "unit": "G L1 accesses/s (TCP_TOTAL_CACHE_ACCESSES)", "frac": round(acc / avg_s / 1e9 / (256 * CLOCK_GHZ), 4),
+              "ta_busy_frac": d.get("ta_busy_frac"), "accesses_per_launch": acc}
+        roof["l1"] = ta
+        if ta["frac"] > roof["frac"]:
+            valu = {k: roof[k] for k in ("unit", "achieved", "peak", "frac", "valu_cycles_per_launch",
+                                         "frac_at_measured_clock", "cycles_by_class", "valu_mix", "peak_basis")}
+            roof.update({"bound": "l1_ta", "unit": ta["unit"], "achieved": ta["achieved"], "peak": ta["peak"],
+                         "frac": ta["frac"], "valu": valu,
+                         "peak_basis": "256 CUs x 2.4 GHz x 1 L1 (TCP) access per clock: TA busy "
+                                       f"{d.get('ta_busy_frac')} of the active cycles (TA_TA_BUSY / GRBM_GUI_ACTIVE)"})
     if roof["valu_lane_util"] is not None:  # issued lanes that do work: idle lanes of a divergent wave do not
-        roof["useful_frac"] = round(roof["frac"] * roof["valu_lane_util"], 4)
+        vf = roof["frac"] if roof["bound"] == "valu" else roof["valu"]["frac"]
+        roof["useful_frac"] = round(vf * roof["valu_lane_util"], 4)
     if d.get("hbm_bytes_per_launch") is not None:
         tb = d["hbm_bytes_per_launch"]
         roof["traffic"] = int(tb)

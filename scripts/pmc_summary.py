@@ -106,6 +106,10 @@ def main():
                            if fam_mean("SQ_WAIT_ANY")[0] and fam_mean("SQ_WAVE_CYCLES")[0] else None),
              "hbm_bytes_per_launch": traffic["bytes_per_launch"] if fetch and write else None,
              "valu_mix": mix_file,
+             # the L1 address path (TA): busy cycles of the 256 CUs' TA units over the GPU's active cycles
+             "ta_busy_frac": (round(fam_mean("TA_TA_BUSY")[0] / (256 * gui / 8), 4)
+                              if fam_mean("TA_TA_BUSY")[0] and gui else None),
+             "tcp_accesses_per_launch": fam_mean("TCP_TOTAL_CACHE_ACCESSES")[0],
              "counters": {c: fam_mean(c)[0] for c in sorted({c for k, cs in acc.items() if k.startswith(fam)
                                                              for c in cs})},
              "formulas": {"valu_issue_frac_measured_clock": "SQ_INSTS_VALU * 2 / (1024 SIMDs * GRBM_GUI_ACTIVE / 8 "

@@ -17,5 +17,7 @@ timeout -k 10 300 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_LDS_BANK_CONFLICT SQ_
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 -d $out/pmc5 -o run --output-format csv -- python3 $B > $out/pmc5.log 2>&1
 # conversions and 64-bit integer instructions (bench.py's VALU issue-cycle model: 4 cycles each)
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT -d $out/pmc6 -o run --output-format csv -- python3 $B > $out/pmc6.log 2>&1
+# the memory pipeline: TA / TD busy cycles and L1 (TCP) accesses against the GPU's active cycles (C4's bound)
+timeout -k 10 300 rocprofv3 --pmc TA_TA_BUSY TD_TD_BUSY TCP_TOTAL_CACHE_ACCESSES TCP_TCC_READ_REQ GRBM_GUI_ACTIVE -d $out/pmc7 -o run --output-format csv -- python3 $B > $out/pmc7.log 2>&1
 key=$(python3 -c "import json; print([json.loads(l) for l in open('$out/trace.log') if l.startswith('{\"metric')][-1]['config']['key'])")
 python3 scripts/pmc_summary.py $out $tag "$key" $out/summary
