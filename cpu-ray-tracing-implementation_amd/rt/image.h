@@ -2,11 +2,13 @@
 //
 // The reference decodes files with stb_image (stbi_loadf: 8-bit formats come back linear, as
 // powf(byte / 255, 2.2)) or tinyexr, then stores bytes with float_to_byte (<= 0 -> 0, >= 1 -> 255,
-// else int(256 v)). Here: baseline JPEG through our own decoder (rt/jpeg.h, byte-identical to the
-// reference's stb_image on the reference's earthmap.jpg), binary/ASCII PPM (P6/P3, 8-bit) and PFM
-// (linear floats). PNG, EXR and progressive JPEG are not decoded; other hosts decode elsewhere and
-// pass linear floats to image(width, height, pixels). As in the reference, a file that cannot be
-// loaded prints an error and leaves a 0 x 0 image, which picture_texture samples as magenta.
+// else int(256 v)). Here: our own decoders, each pinned byte for byte against the reference's stb_image
+// -- baseline JPEG (rt/jpeg.h, incl. the reference's earthmap.jpg), PNG (rt/png.h: all colour types,
+// bit depths and Adam7) and Radiance HDR (rt/hdr.h, linear floats as stbi_loadf returns them) -- plus
+// binary/ASCII PPM (P6/P3, 8-bit) and PFM (linear floats). EXR (tinyexr, not vendored in the reference)
+// and progressive JPEG are not decoded; other hosts decode elsewhere and pass linear floats to
+// image(width, height, pixels). As in the reference, a file that cannot be loaded prints an error and
+// leaves a 0 x 0 image, which picture_texture samples as magenta.
 #pragma once
 #include <cmath>
 #include <cstdint>
@@ -17,7 +19,9 @@
 #include <string>
 #include <vector>
 
+#include "hdr.h"
 #include "jpeg.h"
+#include "png.h"
 
 class image {
  public:
@@ -80,6 +84,31 @@ class image {
   bool load(const std::string& path) {
     std::ifstream in(path, std::ios::binary);
     if (!in) return false;
+    if (in.peek() == 0x89 || in.peek() == '#') {  // PNG signature / Radiance "#?RADIANCE"
+      std::vector<uint8_t> file((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+      std::string err;
+      if (rt_png::is_png(file)) {
+        rt_png::Image im;
+        if (!rt_png::decode(file, im, &err)) {
+          std::cerr << err << "\n";
+          return false;
+        }
+        std::vector<float> f(im.rgb.size());
+        for (size_t i = 0; i < f.size(); i++) f[i] = ldr_to_linear(im.rgb[i]);
+        set(im.width, im.height, f);
+        return !bytes_.empty();
+      }
+      if (rt_hdr::is_hdr(file)) {
+        rt_hdr::Image im;
+        if (!rt_hdr::decode(file, im, &err)) {
+          std::cerr << err << "\n";
+          return false;
+        }
+        set(im.width, im.height, im.rgb);
+        return !bytes_.empty();
+      }
+      return false;
+    }
     if (in.peek() == 0xFF) {  // JPEG (SOI = FF D8)
       std::vector<uint8_t> file((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
       rt_jpeg::Image im;

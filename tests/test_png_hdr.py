@@ -1,0 +1,68 @@
+"""PNG and Radiance HDR decoding for picture textures (rt/png.h, rt/hdr.h through rt/image.h) against the
+reference's own decoder.
+
+The reference loads every non-EXR image through its vendored stb_image (image.h:33-50: stbi_loadf with 3
+components, then float_to_byte). tests/golden/image_golden.json holds md5s of what that decoder returns
+-- built from the reference's stb_image.h where it lies (oracle/ref_stb_decode.cpp,
+tests/golden/make_image_golden.py) -- for PNGs in every colour type, bit depth, filter and interlace mode,
+zlib streams with stored / fixed / dynamic blocks and split IDAT chunks, and HDR files with run-length and
+flat scanlines. Our image class must hold the same texture bytes."""
+import hashlib
+import json
+import os
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+RT = os.path.join(REPO, "cpu-ray-tracing-implementation_amd", "rt")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+with open(os.path.join(GOLDEN, "image_golden.json")) as _f:
+    EXPECTED = json.load(_f)
+FILES = {name: os.path.join(GOLDEN, "images", name) for name in EXPECTED if not name.startswith("_")}
+
+
+@pytest.fixture(scope="module")
+def dump(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("img") / "image_dump")
+    subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-Werror", "-I", RT, "-o", exe,
+                    os.path.join(REPO, "tests", "native", "image_dump.cpp")], check=True)
+
+    def run(path):
+        lines = subprocess.run([exe, path], check=True, capture_output=True, text=True).stdout.split("\n")
+        w, h = map(int, lines[0].split())
+        return w, h, bytes.fromhex(lines[1])
+    return run
+
+
+@pytest.mark.parametrize("name", sorted(FILES))
+def test_texture_bytes_match_the_reference_decoder(dump, name):
+    want = EXPECTED[name]
+    assert want["decodes"]
+    w, h, tex = dump(FILES[name])
+    assert (w, h) == (want["width"], want["height"])
+    assert hashlib.md5(tex).hexdigest() == want["texture_md5"]
+
+
+def test_live_against_the_reference_decoder_when_built(dump):
+    stb = os.path.join(REPO, "oracle", "_ref", "stb_decode")
+    if not os.path.exists(stb):
+        pytest.skip("oracle/_ref/stb_decode not built (no /root/reference here)")
+    for name, path in FILES.items():
+        lines = subprocess.run([stb, path], check=True, capture_output=True, text=True).stdout.split("\n")
+        w, h, tex = dump(path)
+        assert lines[0] == f"{w} {h}" and bytes.fromhex(lines[2]) == tex, name
+
+
+def test_corrupt_files_are_refused(dump, tmp_path):
+    # a truncated or damaged file leaves a 0 x 0 image (picture_texture samples magenta), as in the reference
+    src = open(FILES["rgb8_paeth.png"], "rb").read()
+    for i, bad in enumerate([src[:60], src[:8] + b"\0" * 40, src[:33] + b"\0\0\0\x05IDAT\x78\x9c\xff\xff\xff" + src[-12:]]):
+        p = tmp_path / f"bad{i}.png"
+        p.write_bytes(bad)
+        w, h, tex = dump(str(p))
+        assert (w, h) == (0, 0) and tex == b"", i
+    hdr = open(FILES["rle.hdr"], "rb").read().replace(b"FORMAT=32-bit_rle_rgbe", b"FORMAT=32-bit_rle_xyze")
+    p = tmp_path / "bad.hdr"
+    p.write_bytes(hdr)
+    assert dump(str(p))[:2] == (0, 0)
