@@ -226,7 +226,9 @@ def parity_tiles(fb, W, tiles, ref, rel_tol=None):
     """The GPU framebuffer's pixels of `tiles` against the oracle's (same seed, same sample streams):
     SURVEY.md §8(c) link 3, at the full bench config. fp32: per-channel RMSE < 1e-4 (north_star). fp64
     (rel_tol): also the count of pixels differing by more than rel_tol relative (the -m gpu tests hold
-    fp64 to 1e-9 in all but a few pixels). mean_radiance shows the compared pixels are not black."""
+    fp64 to 1e-9 in all but a few pixels). mean_radiance shows the compared pixels are not black, beside
+    the whole GPU frame's (frame_mean_radiance: the C4 stand-in is a dim scene, its light quad high above
+    the geometry)."""
     from rt_amd.tiling import pixel_index
     idx = torch.from_numpy(pixel_index(tiles, W)).to(fb.device)
     got = fb[idx].double().cpu().numpy()
@@ -235,6 +237,7 @@ def parity_tiles(fb, W, tiles, ref, rel_tol=None):
     out = {"rmse": [float(f"{x:.3g}") for x in rmse], "max_abs": float(f"{np.abs(d).max():.3g}"),
            "tiles": len(tiles), "pixels": int(d.shape[0]), "tolerance": 1e-4,
            "mean_radiance": float(f"{ref.mean():.4g}"), "lit_pixels": int((ref.max(-1) > 1e-3).sum()),
+           "frame_mean_radiance": float(f"{fb.double().mean().item():.4g}"),
            "pass": bool((rmse < 1e-4).all() and np.isfinite(got).all()),
            "against": "oracle fp64, same seed and counter-RNG streams"}
     if rel_tol is not None:

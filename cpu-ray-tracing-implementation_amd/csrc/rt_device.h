@@ -27,6 +27,9 @@ namespace rtd {
 #ifndef RT_WIDE_OCT32  // fp32 rays over the wide BVH: octant-ordered planes, (p - o) * inv (C3 fp32 60.87 ->
 #define RT_WIDE_OCT32 1  // 57.22 ms/frame, C4 351.9 -> 341.6)
 #endif
+#ifndef RT_WIDE_FMA32  // fp32 rays over an LDS tree: one fma per plane distance, three per-ray constants and one
+#define RT_WIDE_FMA32 1  // bound (trace_wide; C3 fp32 49.63 -> 48.54 ms/frame; 2, per-axis constants: 49.01)
+#endif
 #ifndef RT_WIDE_OFS64  // fp64 rays keep 64-bit addresses into trees in HBM (C4 fp64: 32-bit offsets 573.5 ms/frame,
 #define RT_WIDE_OFS64 1  // 64-bit 545.1; fp32 the other way round, 340.7 -> 329.1)
 #endif
@@ -1114,7 +1117,17 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
   // constants cost the fp32 kernels, at their tighter register budgets, more spills than the fmas
   // save (C4 fp32 351 -> 460 ms/frame; fp64 C3 89.8 -> 81.7, C4 561 -> 545), so fp32 keeps
   // (p - o) * inv, octant-ordered (RT_WIDE_OCT32: C3 fp32 60.9 -> 57.2, C4 351.9 -> 341.6).
-  constexpr bool kFma = F64 && RT_WIDE_FMA, kOct = kFma || (!F64 && RT_WIDE_OCT32);
+  // RT_WIDE_FMA32 (round 4): fp32 rays form p * inv + c too, with c = -o * inv rounded and ONE per-ray
+  // bound instead of six constants: each distance is within |o_a * inv_a| 2^-24 of (p - o) * inv
+  // (c's rounding; the fma's own is relative, covered by box_slack), so the test tn <= tf * slack +
+  // 2 e with e = max_a |o_a inv_a| 2^-23 accepts every box the exact test accepts. An infinite or NaN
+  // o_a * inv_a (a zero direction component) gives planes of the right sign or NaN, and no bound.
+  // Over a tree in HBM (C4 stand-in) the one bound culls too little: a ray with a small direction
+  // component has a large o_a * inv_a, and the bound then widens every axis (C4 fp32 310.7 -> 378.5
+  // ms/frame; C3 49.8 -> 48.8). RT_WIDE_FMA32=2: per-axis constants, as the fp64 rays'.
+  constexpr bool kFma = (F64 && RT_WIDE_FMA) || (!F64 && LDSN && RT_WIDE_FMA32 == 2);
+  constexpr bool kFma32 = !F64 && LDSN && RT_WIDE_FMA32 == 1;
+  constexpr bool kOct = kFma || kFma32 || (!F64 && RT_WIDE_OCT32);
   [[maybe_unused]] const uint32_t onx0 = (__float_as_uint(inv.x) >> 31) * 48u,
                                  ony0 = 16u + (__float_as_uint(inv.y) >> 31) * 48u,
                                  onz0 = 32u + (__float_as_uint(inv.z) >> 31) * 48u;
@@ -1132,6 +1145,16 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
     cpair(o.x, inv.x, wx, cnx, cfx);
     cpair(o.y, inv.y, wy, cny, cfy);
     cpair(o.z, inv.z, wz, cnz, cfz);
+  }
+  [[maybe_unused]] float e2 = 0.f;  // kFma32: twice the bound e
+  if constexpr (kFma32) {
+    auto cterm = [](float oa, float ia, float& c) {
+      const float oi = oa * ia;
+      c = -oi;
+      return fabsf(oi) < Num<float>::inf() ? fabsf(oi) : 0.f;
+    };
+    const float m = fmaxf(fmaxf(cterm(o.x, inv.x, cnx), cterm(o.y, inv.y, cny)), cterm(o.z, inv.z, cnz));
+    e2 = m * 2.384185791015625e-07f;  // 2^-22
   }
   // the four children's sort keys (bits(t_near) with the slot in the low 2 bits; 0xFFFFFFFF: missed)
   // of the float node at nb (LDS or HBM)
@@ -1165,6 +1188,10 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
         if constexpr (kFma) {
           tn = fmaxf(fmaxf(fmaf(px, inv.x, cnx), fmaf(py, inv.y, cny)), fmaxf(fmaf(pz, inv.z, cnz), tmin_box));
           tf = fminf(fminf(fmaf(qx, inv.x, cfx), fmaf(qy, inv.y, cfy)), fminf(fmaf(qz, inv.z, cfz), tmx));
+        } else if constexpr (kFma32) {
+          tn = fmaxf(fmaxf(fmaf(px, inv.x, cnx), fmaf(py, inv.y, cny)), fmaxf(fmaf(pz, inv.z, cnz), tmin_box));
+          tf = fminf(fminf(fmaf(qx, inv.x, cnx), fmaf(qy, inv.y, cny)), fminf(fmaf(qz, inv.z, cnz), tmx));
+          return keyof(tn, fmaf(tf, Num<float>::box_slack(), e2), c);
         } else {
           tn = fmaxf(fmaxf((px - o.x) * inv.x, (py - o.y) * inv.y), fmaxf((pz - o.z) * inv.z, tmin_box));
           tf = fminf(fminf((qx - o.x) * inv.x, (qy - o.y) * inv.y), fminf((qz - o.z) * inv.z, tmx));
