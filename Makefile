@@ -20,7 +20,7 @@ CXX      ?= g++
 CXXFLAGS ?= -O2 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter
 RT_HDRS  := $(wildcard $(PKG)/rt/*.h) include/rt_hip.h
 
-all: $(BUILD)/librt_hip.so $(BUILD)/librt_scenes.so $(BUILD)/rt_main tools/valu_rates oracle
+all: $(BUILD)/librt_hip.so $(BUILD)/librt_scenes.so $(BUILD)/rt_main tools/valu_rates tools/l1_rates oracle
 
 # one object per source, so a host-only change does not recompile the kernels
 LIB_OBJS := $(BUILD)/obj/rt_kernels.o $(BUILD)/obj/rt_multi.o $(BUILD)/obj/scene_compile.o
@@ -61,6 +61,9 @@ $(BUILD)/rt_main: examples/main.cc $(PKG)/scenes/config_scenes.cpp $(PKG)/scenes
 
 # measurement tool: issue cost of single VALU opcodes (scripts/valu_rates.sh, bench.py's fp64 roofline)
 tools/valu_rates: tools/valu_rates.hip
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -o $@ $<
+# measurement tool: L1 (TA/TD) cost of a vector load by width, active lanes and address pattern
+tools/l1_rates: tools/l1_rates.hip
 	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -o $@ $<
 
 oracle:

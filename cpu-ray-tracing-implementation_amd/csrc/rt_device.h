@@ -27,6 +27,9 @@ namespace rtd {
 #ifndef RT_WIDE_OCT32  // fp32 rays over the wide BVH: octant-ordered planes, (p - o) * inv (C3 fp32 60.87 ->
 #define RT_WIDE_OCT32 1  // 57.22 ms/frame, C4 351.9 -> 341.6)
 #endif
+#ifndef RT_WIDE_HALF  // trees in HBM: read from the fp16 octant copies (rt_scene.h WNodeH), 5 loads per node visit
+#define RT_WIDE_HALF 0
+#endif
 #ifndef RT_WIDE_FMA32  // fp32 rays over an LDS tree: one fma per plane distance, three per-ray constants and one
 #define RT_WIDE_FMA32 1  // bound (trace_wide; C3 fp32 49.63 -> 48.54 ms/frame; 2, per-axis constants: 49.01)
 #endif
@@ -383,6 +386,7 @@ struct DevScene {
   uint32_t n_wnodes, n_wprim_words, wroot, wide_stack, wide_kinds;
   int32_t has_wide;
   uint32_t wide_big;  // primitives at the head of the word stream, tested before the tree
+  const WNodeH* wnodesh;  // the half-precision octant copies (0: none; RT_WIDE_HALF)
   // a tree in HBM keeps at most kWideLdsStack stack entries per lane in LDS; deeper entries (rare:
   // every child of every node on a path hit) go to wide_spill[(depth - kWideLdsStack) * spill_lanes + lane]
   uint32_t* wide_spill;
@@ -1225,6 +1229,76 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
       k3 = slab(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, 3u);
     }
   };
+  // RT_WIDE_HALF: the keys of node c from the ray's octant copy (rt_scene.h WNodeH), and its child codes.
+  // A plane's distance is one fma of its fp16 offset (v_fma_mix_f32): h * inv + b, b = (origin - o) *
+  // inv per node and axis. b carries two roundings, |b| 2^-23 at most: the near planes take b - e and
+  // the far ones b + e, e = |b| 2^-22 (+ the fp64 ray's widening w), so no box the float node would
+  // enter is culled; the fma's own rounding is relative, covered by box_slack like the float path's.
+  constexpr bool kHalf = !LDSN && RT_WIDE_HALF;
+  [[maybe_unused]] const unsigned char* hbase = nullptr;
+  [[maybe_unused]] uint32_t hoct = 0;  // byte offset of the ray's octant copy
+  // RT_WIDE_HALF=2: one copy (octant 0: lo planes in nr, hi in fr) and the near / far words picked per
+  // axis by v_perm_b32 with a per-ray selector (sel*: 0x07060504 takes the hi word, 0x03020100 the lo)
+  [[maybe_unused]] uint32_t selx = 0, sely = 0, selz = 0;
+  if constexpr (kHalf) {
+    hbase = (const unsigned char*)sc.wnodesh;
+    if constexpr (RT_WIDE_HALF == 2) {
+      selx = (__float_as_uint(inv.x) >> 31) ? 0x07060504u : 0x03020100u;
+      sely = (__float_as_uint(inv.y) >> 31) ? 0x07060504u : 0x03020100u;
+      selz = (__float_as_uint(inv.z) >> 31) ? 0x07060504u : 0x03020100u;
+    } else {
+      const uint32_t oc = (__float_as_uint(inv.x) >> 31) | (__float_as_uint(inv.y) >> 31) << 1 |
+                          (__float_as_uint(inv.z) >> 31) << 2;
+      hoct = oc * sc.n_wnodes * (uint32_t)sizeof(WNodeH);
+    }
+  }
+  [[maybe_unused]] auto half_keys = [&](uint32_t c, uint32_t& k0, uint32_t& k1, uint32_t& k2, uint32_t& k3, uint4& cc) {
+    const unsigned char* hp = hbase + (hoct + c * (uint32_t)sizeof(WNodeH));
+    const uint4 h0 = *(const uint4*)hp;
+    uint4 h1 = *(const uint4*)(hp + 16), h2 = *(const uint4*)(hp + 32), h3 = *(const uint4*)(hp + 48);
+    cc = *(const uint4*)(hp + 64);
+    if constexpr (RT_WIDE_HALF == 2) {  // lo: x h1.xy, y h1.zw, z h2.xy; hi: x h2.zw, y h3.xy, z h3.zw
+      auto pick = [](uint32_t& lo, uint32_t& hi, uint32_t sel) {
+        const uint32_t n = __builtin_amdgcn_perm(hi, lo, sel), f = __builtin_amdgcn_perm(lo, hi, sel);
+        lo = n;
+        hi = f;
+      };
+      pick(h1.x, h2.z, selx);
+      pick(h1.y, h2.w, selx);
+      pick(h1.z, h3.x, sely);
+      pick(h1.w, h3.y, sely);
+      pick(h2.x, h3.z, selz);
+      pick(h2.y, h3.w, selz);
+    }
+    const float tmx = (float)tmax;
+    auto bounds = [](float org, float oa, float iv, float wa, float& bn, float& bf) {
+      const float b = (org - oa) * iv;
+      const float e = fmaf(fabsf(b), 2.384185791015625e-07f, wa);  // 2^-22
+      bn = b - e;
+      bf = b + e;
+    };
+    float bnx, bfx, bny, bfy, bnz, bfz;
+    bounds(__uint_as_float(h0.x), o.x, inv.x, wx, bnx, bfx);
+    bounds(__uint_as_float(h0.y), o.y, inv.y, wy, bny, bfy);
+    bounds(__uint_as_float(h0.z), o.z, inv.z, wz, bnz, bfz);
+    auto H = [](uint32_t w, bool hi) {
+      return (float)__builtin_bit_cast(_Float16, (uint16_t)(hi ? (w >> 16) : (w & 0xFFFFu)));
+    };
+    // nr: x h1.x h1.y, y h1.z h1.w, z h2.x h2.y; fr: x h2.z h2.w, y h3.x h3.y, z h3.z h3.w
+    auto key = [&](uint32_t nx, uint32_t ny, uint32_t nz, uint32_t fx, uint32_t fy, uint32_t fz, bool hi,
+                   uint32_t slot) {
+      const float tn = fmaxf(fmaxf(fmaf(H(nx, hi), inv.x, bnx), fmaf(H(ny, hi), inv.y, bny)),
+                             fmaxf(fmaf(H(nz, hi), inv.z, bnz), tmin_box));
+      const float tf = fminf(fminf(fmaf(H(fx, hi), inv.x, bfx), fmaf(H(fy, hi), inv.y, bfy)),
+                             fminf(fmaf(H(fz, hi), inv.z, bfz), tmx)) *
+                       Num<float>::box_slack();
+      return tn <= tf ? ((__float_as_uint(tn) & ~3u) | slot) : 0xFFFFFFFFu;
+    };
+    k0 = key(h1.x, h1.z, h2.x, h2.z, h3.x, h3.z, false, 0u);
+    k1 = key(h1.x, h1.z, h2.x, h2.z, h3.x, h3.z, true, 1u);
+    k2 = key(h1.y, h1.w, h2.y, h2.w, h3.y, h3.w, false, 2u);
+    k3 = key(h1.y, h1.w, h2.y, h2.w, h3.y, h3.w, true, 3u);
+  };
   // the primitives of a leaf (or of the head list), their records from word w on
   // a primitive word by 32-bit byte offset from the base (one VGPR of address; see node_keys)
   auto pw = [&](uint32_t k) -> WW {
@@ -1293,11 +1367,16 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
         }
         cur = pop();
       } else {
-        const OfsT nof = node_off(cur);
         uint4 cc{};
         uint32_t k0, k1, k2, k3;
-        if constexpr (!LDSN) cc = *(const uint4*)(nbase + (nof + 96u));
-        node_keys(nof, k0, k1, k2, k3);
+        [[maybe_unused]] OfsT nof{};
+        if constexpr (kHalf) {
+          half_keys(cur, k0, k1, k2, k3, cc);
+        } else {
+          nof = node_off(cur);
+          if constexpr (!LDSN) cc = *(const uint4*)(nbase + (nof + 96u));
+          node_keys(nof, k0, k1, k2, k3);
+        }
         auto child = [&](uint32_t k) -> uint32_t {
           if constexpr (LDSN) {
             return ((const uint16_t*)(nbase + (nof + 96u)))[k & 3u];
@@ -1357,7 +1436,13 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
       // live through the slab tests and the sort, which spilled: C3 76.4 -> 81.5 ms/frame). Tree in HBM:
       // all four come with the boxes, one latency instead of one per push (C4 462 -> 421 ms/frame).
       uint4 cc{};
-      if constexpr (!LDSN) cc = *(const uint4*)(nbase + (nof + 96u));
+      uint32_t k0, k1, k2, k3;
+      if constexpr (kHalf) {
+        half_keys(cur, k0, k1, k2, k3, cc);
+      } else {
+        if constexpr (!LDSN) cc = *(const uint4*)(nbase + (nof + 96u));
+        node_keys(nof, k0, k1, k2, k3);
+      }
       auto child = [&](uint32_t k) -> uint32_t {
         if constexpr (LDSN) {
           return ((const uint16_t*)(nbase + (nof + 96u)))[k & 3u];
@@ -1366,8 +1451,6 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
           return sl == 0 ? cc.x : (sl == 1 ? cc.y : (sl == 2 ? cc.z : cc.w));
         }
       };
-      uint32_t k0, k1, k2, k3;
-      node_keys(nof, k0, k1, k2, k3);
 #define RT_CS(a, b)                 \
   {                                 \
     const uint32_t lo_ = min(a, b); \

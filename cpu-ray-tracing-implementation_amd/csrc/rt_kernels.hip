@@ -1638,6 +1638,7 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
   s.wide_stack = h.wide_stack;
   s.wide_kinds = h.wide_kinds;
   s.wide_big = h.wide_big;
+  s.wnodesh = h.has_wnodesh ? (const WNodeH*)at(h.off_wnodesh) : nullptr;
   return s;
 }
 

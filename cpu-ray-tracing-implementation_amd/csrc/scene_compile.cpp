@@ -631,6 +631,77 @@ inline float up(double x) {
   return std::nextafter(f, std::numeric_limits<float>::infinity());
 }
 
+// fp16 bit patterns of non-negative values (rt_scene.h WNodeH): the value of a pattern, and the
+// largest pattern at or below x / the smallest at or above x (patterns 0 .. 0x7C00 = +inf order like
+// their values)
+inline double half_value(uint16_t h) {
+  const int e = (h >> 10) & 31, m = h & 1023;
+  if (e == 31) return std::numeric_limits<double>::infinity();
+  return e == 0 ? std::ldexp((double)m, -24) : std::ldexp((double)(1024 + m), e - 25);
+}
+inline uint16_t half_down(double x) {
+  if (!(x >= 0)) return 0;
+  uint32_t lo = 0, hi = 0x7C00;  // half_value(lo) <= x
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) / 2;
+    (half_value((uint16_t)mid) <= x ? lo : hi) = mid;
+  }
+  return (uint16_t)(half_value((uint16_t)hi) <= x ? hi : lo);
+}
+inline uint16_t half_up(double x) {
+  if (!(x > 0)) return 0;
+  uint32_t lo = 0, hi = 0x7C00;  // half_value(hi) >= x
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) / 2;
+    (half_value((uint16_t)mid) >= x ? hi : lo) = mid;
+  }
+  return (uint16_t)hi;
+}
+// The eight octant copies of a wide tree in WNodeH form (rt_scene.h): copy o, node i at o * n + i.
+// The float node's planes are already rounded outward; the offsets from the origin (float minus float:
+// exact in double) are rounded outward again to fp16.
+std::vector<WNodeH> half_octant_nodes(const std::vector<WNode>& wn) {
+  const size_t n = wn.size();
+  std::vector<WNodeH> out(8 * n);
+  for (size_t i = 0; i < n; i++) {
+    const WNode& w = wn[i];
+    const float* lo[3] = {w.lox, w.loy, w.loz};
+    const float* hi[3] = {w.hix, w.hiy, w.hiz};
+    float org[3];
+    for (int a = 0; a < 3; a++) {
+      float m = std::numeric_limits<float>::infinity();
+      for (int c = 0; c < 4; c++)
+        if (std::isfinite(lo[a][c])) m = std::min(m, lo[a][c]);
+      org[a] = std::isfinite(m) ? m : 0.f;
+    }
+    uint16_t qlo[3][4], qhi[3][4];
+    for (int a = 0; a < 3; a++)
+      for (int c = 0; c < 4; c++) {
+        const bool used = std::isfinite(lo[a][c]) && std::isfinite(hi[a][c]);
+        qlo[a][c] = used ? half_down((double)lo[a][c] - (double)org[a]) : (uint16_t)0x7C00;
+        qhi[a][c] = used ? half_up((double)hi[a][c] - (double)org[a]) : (uint16_t)0x7C00;
+      }
+    for (int o = 0; o < 8; o++) {
+      WNodeH& h = out[(size_t)o * n + i];
+      h.ox = org[0];
+      h.oy = org[1];
+      h.oz = org[2];
+      h.pad = 0;
+      for (int a = 0; a < 3; a++) {
+        const bool neg = (o >> a) & 1;  // a negative direction on axis a enters through the hi plane
+        const uint16_t* nq = neg ? qhi[a] : qlo[a];
+        const uint16_t* fq = neg ? qlo[a] : qhi[a];
+        for (int k = 0; k < 2; k++) {
+          h.nr[2 * a + k] = (uint32_t)nq[2 * k] | (uint32_t)nq[2 * k + 1] << 16;
+          h.fr[2 * a + k] = (uint32_t)fq[2 * k] | (uint32_t)fq[2 * k + 1] << 16;
+        }
+      }
+      for (int c = 0; c < 4; c++) h.child[c] = w.child[c];
+    }
+  }
+  return out;
+}
+
 template <class D, class S>
 void cvt3(D* d, const S* s) {
   for (int k = 0; k < 3; k++) d[k] = (D)s[k];
@@ -1270,9 +1341,12 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
   words.push_back({0.f, 0.f, 0.f, 0.f});
   words64.push_back({0, 0, 0, 0});
   words64.push_back({0, 0, 0, 0});
+  const std::vector<WNodeH> wh = half_octant_nodes(wn);
   {  // the fp64 blob: the same float nodes, the double words
     SceneHeader& h = out->hdr64;
     h.off_wnodes = append(out->blob64, wn);
+    h.off_wnodesh = append(out->blob64, wh);
+    h.has_wnodesh = 1;
     h.off_wprims = append(out->blob64, words64);
     out->blob64.resize((out->blob64.size() + 255) & ~size_t(255));
     h.bytes = out->blob64.size();
@@ -1286,6 +1360,8 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
   }
   SceneHeader& h = out->hdr;
   h.off_wnodes = append(out->blob32, wn);
+  h.off_wnodesh = append(out->blob32, wh);
+  h.has_wnodesh = 1;
   h.off_wprims = append(out->blob32, words);
   out->blob32.resize((out->blob32.size() + 255) & ~size_t(255));
   h.bytes = out->blob32.size();

@@ -199,6 +199,158 @@ __device__ __forceinline__ void body(double& a0, double& a1, double& a2, double&
 #define X(r) { asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(f##r) : "v"(fb), "s"(m)); }
       X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
 #undef X
+    } else if constexpr (K == 41) {
+#define X(r) asm volatile("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,0,0]" : "+v"(f##r) : "v"(fb), "v"(fc));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 42) {
+#define X(r) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(f##r) : "v"(fb), "s"((uint32_t)0x07060100u));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 43) {
+#define X(r) asm volatile("v_max3_f32 %0, %0, %1, %2" : "+v"(f##r) : "v"(fb), "v"(fc));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 44) {
+#define X(r) asm volatile("v_cvt_f32_ubyte1 %0, %0" : "+v"(f##r));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 45) {
+#define X(r) asm volatile("v_min_u32 %0, %0, %1" : "+v"(f##r) : "v"(fb));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 46) {
+#define X(r) asm volatile("v_and_or_b32 %0, %0, %1, %2" : "+v"(f##r) : "v"(fb), "v"(fc));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 47) {
+#define X(r) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(f##r) : "v"(fb), "v"(fc));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 48) {
+#define X(r) asm volatile("v_lshl_add_u32 %0, %0, %1, %2" : "+v"(f##r) : "v"(fb), "v"(fc));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 49) {
+#define X(r) asm volatile("v_lshl_or_b32 %0, %0, %1, %2" : "+v"(f##r) : "v"(fb), "v"(fc));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 50) {
+#define X(r) asm volatile("v_or3_b32 %0, %0, %1, %2" : "+v"(f##r) : "v"(fb), "v"(fc));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 51) {
+#define X(r) asm volatile("v_max3_u32 %0, %0, %1, %2" : "+v"(f##r) : "v"(fb), "v"(fc));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 52) {
+#define X(r) asm volatile("v_min3_f32 %0, %0, %1, %2" : "+v"(f##r) : "v"(fb), "v"(fc));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 53) {
+#define X(r) asm volatile("v_med3_f32 %0, %0, %1, %2" : "+v"(f##r) : "v"(fb), "v"(fc));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 54) {
+#define X(r) asm volatile("v_mad_u32_u24 %0, %0, %1, %2" : "+v"(f##r) : "v"(fb), "v"(fc));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 55) {
+#define X(r) asm volatile("v_bfi_b32 %0, %0, %1, %2" : "+v"(f##r) : "v"(fb), "v"(fc));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 56) {
+#define X(r) asm volatile("v_alignbit_b32 %0, %0, %1, %2" : "+v"(f##r) : "v"(fb), "v"(fc));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 57) {
+#define X(r) asm volatile("v_xad_u32 %0, %0, %1, %2" : "+v"(f##r) : "v"(fb), "v"(fc));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 58) {
+#define X(r) asm volatile("v_max_u32 %0, %0, %1" : "+v"(f##r) : "v"(fb));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 59) {
+#define X(r) asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(f##r) : "v"(fb));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 60) {
+#define X(r) asm volatile("v_sub_u32 %0, %0, %1" : "+v"(f##r) : "v"(fb));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 61) {
+#define X(r) asm volatile("v_and_b32 %0, %0, %1" : "+v"(f##r) : "v"(fb));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 62) {
+#define X(r) asm volatile("v_or_b32 %0, %0, %1" : "+v"(f##r) : "v"(fb));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 63) {
+#define X(r) asm volatile("v_ldexp_f32 %0, %0, %1" : "+v"(f##r) : "v"(fb));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 64) {
+#define X(r) asm volatile("v_sub_f32 %0, %0, %1" : "+v"(f##r) : "v"(fb));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 65) {
+#define X(r) asm volatile("v_max_i32 %0, %0, %1" : "+v"(f##r) : "v"(fb));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 66) {
+#define X(r) asm volatile("v_lshlrev_b32 %0, %0, %1" : "+v"(f##r) : "v"(fb));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 67) {
+#define X(r) asm volatile("v_ashrrev_i32 %0, %0, %1" : "+v"(f##r) : "v"(fb));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 68) {
+#define X(r) asm volatile("v_mul_hi_u32_u24 %0, %0, %1" : "+v"(f##r) : "v"(fb));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 69) {
+#define X(r) asm volatile("v_max_f32 %0, %0, %1" : "+v"(f##r) : "v"(fb));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 70) {
+#define X(r) asm volatile("v_not_b32 %0, %0" : "+v"(f##r));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 71) {
+#define X(r) asm volatile("v_cvt_f32_f16 %0, %0" : "+v"(f##r));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 72) {
+#define X(r) asm volatile("v_cvt_u32_f32 %0, %0" : "+v"(f##r));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 73) {
+#define X(r) asm volatile("v_cvt_i32_f32 %0, %0" : "+v"(f##r));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 74) {
+#define X(r) asm volatile("v_fract_f32 %0, %0" : "+v"(f##r));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 75) {
+#define X(r) asm volatile("v_floor_f32 %0, %0" : "+v"(f##r));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 76) {
+#define X(r) asm volatile("v_trunc_f32 %0, %0" : "+v"(f##r));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 77) {
+#define X(r) asm volatile("v_rndne_f32 %0, %0" : "+v"(f##r));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 78) {
+#define X(r) asm volatile("v_cvt_f16_f32 %0, %0" : "+v"(f##r));
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
     } else if constexpr (K == 19) {
 #define X(r) { uint64_t t; asm volatile("v_cmp_class_f64_e64 %0, %1, %2" : "=s"(t) : "v"(a##r), "v"(f0)); s##r ^= t; }
       X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
@@ -242,7 +394,17 @@ int main() {
       {"v_mul_lo_u32", k_rate<15>},    {"v_ldexp_f64", k_rate<16>},      {"v_lshlrev_b64", k_rate<17>},
       {"v_rsq_f32", k_rate<18>},       {"v_cmp_class_f64", k_rate<19>},  {"v_pk_fma_f32", k_rate<20>},
       {"v_mul_f32", k_rate<21>},       {"v_xor_b32", k_rate<22>},
-      {"v_mov_b32", k_rate<23>}, {"v_cndmask_b32_vcc", k_rate<24>}, {"v_cmp_lt_f32", k_rate<25>}, {"v_add_u32", k_rate<26>}, {"v_lshrrev_b32", k_rate<27>}, {"v_bfe_u32", k_rate<28>}, {"v_mad_u64_u32", k_rate<29>}, {"v_min_f32", k_rate<30>}, {"v_readfirstlane_b32", k_rate<31>}, {"v_fract_f64", k_rate<32>}, {"v_rsq_f64", k_rate<33>}, {"v_sqrt_f32", k_rate<34>}, {"v_mul_hi_u32", k_rate<35>}, {"v_cvt_f32_u32", k_rate<36>}, {"v_min_f64", k_rate<37>}, {"v_cmp_eq_u32", k_rate<38>}, {"v_bitop3_b32", k_rate<39>}, {"v_cndmask_b32_e64_v", k_rate<40>}, 
+      {"v_mov_b32", k_rate<23>}, {"v_cndmask_b32_vcc", k_rate<24>}, {"v_cmp_lt_f32", k_rate<25>}, {"v_add_u32", k_rate<26>}, {"v_lshrrev_b32", k_rate<27>}, {"v_bfe_u32", k_rate<28>}, {"v_mad_u64_u32", k_rate<29>}, {"v_min_f32", k_rate<30>}, {"v_readfirstlane_b32", k_rate<31>}, {"v_fract_f64", k_rate<32>}, {"v_rsq_f64", k_rate<33>}, {"v_sqrt_f32", k_rate<34>}, {"v_mul_hi_u32", k_rate<35>}, {"v_cvt_f32_u32", k_rate<36>}, {"v_min_f64", k_rate<37>}, {"v_cmp_eq_u32", k_rate<38>}, {"v_bitop3_b32", k_rate<39>}, {"v_cndmask_b32_e64_v", k_rate<40>},
+      {"v_fma_mix_f32", k_rate<41>}, {"v_perm_b32", k_rate<42>}, {"v_max3_f32", k_rate<43>}, {"v_cvt_f32_ubyte1", k_rate<44>},
+      {"v_min_u32", k_rate<45>}, {"v_and_or_b32", k_rate<46>},
+      {"v_add3_u32", k_rate<47>}, {"v_lshl_add_u32", k_rate<48>}, {"v_lshl_or_b32", k_rate<49>}, {"v_or3_b32", k_rate<50>},
+      {"v_max3_u32", k_rate<51>}, {"v_min3_f32", k_rate<52>}, {"v_med3_f32", k_rate<53>}, {"v_mad_u32_u24", k_rate<54>},
+      {"v_bfi_b32", k_rate<55>}, {"v_alignbit_b32", k_rate<56>}, {"v_xad_u32", k_rate<57>}, {"v_max_u32", k_rate<58>},
+      {"v_mul_u32_u24", k_rate<59>}, {"v_sub_u32", k_rate<60>}, {"v_and_b32", k_rate<61>}, {"v_or_b32", k_rate<62>},
+      {"v_ldexp_f32", k_rate<63>}, {"v_sub_f32", k_rate<64>}, {"v_max_i32", k_rate<65>}, {"v_lshlrev_b32", k_rate<66>},
+      {"v_ashrrev_i32", k_rate<67>}, {"v_mul_hi_u32_u24", k_rate<68>}, {"v_max_f32", k_rate<69>}, {"v_not_b32", k_rate<70>},
+      {"v_cvt_f32_f16", k_rate<71>}, {"v_cvt_u32_f32", k_rate<72>}, {"v_cvt_i32_f32", k_rate<73>}, {"v_fract_f32", k_rate<74>},
+      {"v_floor_f32", k_rate<75>}, {"v_trunc_f32", k_rate<76>}, {"v_rndne_f32", k_rate<77>}, {"v_cvt_f16_f32", k_rate<78>},
   };
   int ncu = 0;
   CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
