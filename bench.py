@@ -33,13 +33,16 @@ SIMDS, CLOCK_GHZ = 1024, 2.4  # 256 CUs x 4 SIMDs; the 2.4 GHz peak engine clock
 CYCLE_PEAK_G = SIMDS * CLOCK_GHZ  # G SIMD-cycles/s: every SIMD issuing VALU work every cycle
 # VALU roofline: SIMD cycles per launch = sum over the kernel's VALU instructions of the cycles
 # each holds its SIMD, measured on this MI355X for single opcodes (tools/valu_rates.hip, 8 waves/SIMD, 8
-# independent chains; kernel time x the measured shader clock: profiles/r04c_valu_rates.json) and rounded to
-# the issue cost they show: 2 cycles per wave64 instruction for 32-bit add/mul/fma/logic/moves (measured
-# 2.2-2.4), 4 for every fp64 operation (add/mul/fma/min/max/floor/fract/ldexp), 64-bit moves and shifts,
-# conversions, bit-field extracts, 32-bit integer multiplies, fp32 min/max and v_cndmask with an SGPR mask
-# (4.1-4.3), 4.6 for compares into an SGPR mask (VOPC, any width: 4.7-4.9), 4.8 for v_mad_u64_u32 (5.0),
-# 5.7 for v_readfirstlane (5.9), 8 for fp32 transcendentals (8.1) and 16 for fp64 ones (v_rcp_f64 /
-# v_rsq_f64: 16.2).
+# independent chains; kernel time x the measured shader clock: profiles/r04t_valu_rates.json, 79 opcodes) and
+# rounded to the issue cost they show: 2 cycles per wave64 instruction for 32-bit add/sub/mul/fma, and/or/
+# xor/not/bitop3, moves and right shifts (measured 2.2-2.4); 4 for every fp64 operation, 64-bit moves and
+# shifts, conversions, min/max/med3 of any type, the three-operand integer ops (add3, lshl_add, lshl_or,
+# or3, and_or, xad, perm, bfi, alignbit, mad/mul_u32_u24), 32-bit integer multiplies, left shifts,
+# bit-field extracts, fp32 floor/fract/ldexp, v_fma_mix and v_cndmask with an SGPR mask (4.1-4.3); 4.7 for
+# compares into an SGPR mask (VOPC, any width); 5.0 for v_mad_u64_u32, 5.9 for v_readfirstlane, 8 for fp32
+# transcendentals (8.1) and 16 for fp64 ones (16.2). Opcodes the table measured take their rounded
+# measurement; the others the rules in opcode_cycles.
+VALU_RATES = os.path.join(REPO, "profiles", "r04t_valu_rates.json")
 VALU_PMC_CLASSES = {  # SQ_INSTS_VALU_* class counters -> the static-mix class they count
     "f64_addmulfma": ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64"),
     "f64_trans": ("SQ_INSTS_VALU_TRANS_F64",),
@@ -49,21 +52,47 @@ VALU_PMC_CLASSES = {  # SQ_INSTS_VALU_* class counters -> the static-mix class t
 }
 
 
+_MEASURED = None
+
+
+def _round_cost(c):
+    """A measured cycles-per-instruction figure (event time, so a few % over the issue cost) -> the cost."""
+    for lo, cost in ((14.0, 16.0), (7.0, 8.0), (5.5, 5.9), (4.9, 5.0), (4.5, 4.7), (3.0, 4.0)):
+        if c >= lo:
+            return cost
+    return 2.0
+
+
 def opcode_cycles(op):
     """Issue cycles of one wave64 VALU opcode on gfx950 (the table above)."""
     import re
+    global _MEASURED
+    if _MEASURED is None:
+        _MEASURED = {}
+        if os.path.exists(VALU_RATES):
+            with open(VALU_RATES) as f:
+                for name, v in json.load(f)["per_wave_instr"].items():
+                    if name.startswith("v_cndmask"):  # the table's v_cndmask rows time mask set-up too
+                        continue
+                    _MEASURED[name] = _round_cost(v["cycles_event"])
+    base = re.sub(r"_(e32|e64|sdwa|dpp)$", "", op)
+    if base in _MEASURED:
+        return _MEASURED[base]
     if re.match(r"v_(rcp|rsq|sqrt|exp|log|sin|cos)_f64", op):
         return 16.0
     if re.match(r"v_(rcp|rsq|sqrt|exp|log|sin|cos|rcp_iflag)_f32", op):
         return 8.0
     if op.startswith("v_cmp"):
-        return 4.6
+        return 4.7
     if op.startswith(("v_mad_u64_u32", "v_mad_i64_i32")):
-        return 4.8
+        return 5.0
     if op.startswith(("v_readfirstlane", "v_readlane", "v_writelane")):
-        return 5.7
+        return 5.9
     if ("f64" in op or "_b64" in op or "_u64" in op or "_i64" in op or op.startswith(("v_cvt", "v_bfe", "v_pk_"))
-            or re.match(r"v_mul_(lo|hi)_", op) or re.match(r"v_(min|max|med3)_f32", op)
+            or re.match(r"v_mul_(lo|hi)_", op) or re.match(r"v_(min|max|med3|min3|max3)_", op)
+            or re.match(r"v_(add3|lshl_add|lshl_or|or3|and_or|xad|perm|bfi|alignbit|mad_u32_u24|mad_i32_i24|"
+                        r"mul_u32_u24|mul_i32_i24|mul_hi_u32_u24|ldexp|fract|floor|ceil|trunc|rndne|fma_mix|"
+                        r"mad_mix|lshlrev_b32|sad)", op)
             or op.startswith("v_cndmask_b32_e64")):
         return 4.0
     return 2.0

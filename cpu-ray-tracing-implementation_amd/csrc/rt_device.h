@@ -27,8 +27,8 @@ namespace rtd {
 #ifndef RT_WIDE_OCT32  // fp32 rays over the wide BVH: octant-ordered planes, (p - o) * inv (C3 fp32 60.87 ->
 #define RT_WIDE_OCT32 1  // 57.22 ms/frame, C4 351.9 -> 341.6)
 #endif
-#ifndef RT_WIDE_HALF  // trees in HBM: read from the fp16 octant copies (rt_scene.h WNodeH), 5 loads per node visit
-#define RT_WIDE_HALF 0
+#ifndef RT_WIDE_HALF_F64  // fp64 rays over trees in HBM read the fp16 node form (rt_scene.h WNodeH): 5 loads per
+#define RT_WIDE_HALF_F64 1  // node visit instead of 7 (C4 fp64 504.0 -> 480.8 ms/frame; fp32 rays lose, see WNodeH)
 #endif
 #ifndef RT_WIDE_FMA32  // fp32 rays over an LDS tree: one fma per plane distance, three per-ray constants and one
 #define RT_WIDE_FMA32 1  // bound (trace_wide; C3 fp32 49.63 -> 48.54 ms/frame; 2, per-axis constants: 49.01)
@@ -38,6 +38,12 @@ namespace rtd {
 #endif
 #ifndef RT_WIDE_PREFETCH  // a triangle's words loaded with the record's first word (C4 358.9 -> 357.2 ms)
 #define RT_WIDE_PREFETCH 1
+#endif
+// RT_FLAT_BOX_FMA_F64: fp64 flat boxes with plane distances as fma(p, inv, -o * inv) (flat_slab). Off: it
+// saves 1.5 % (C2 fp64 32.13 -> 31.65 ms/frame) but moves box distances by an ulp and edge decisions with
+// them -- 9 of 364,800 full-size C2 pixels beyond 1e-9 of the oracle instead of 0, row RMSE 2e-16 -> 1e-6
+#ifndef RT_FLAT_BOX_FMA_F64
+#define RT_FLAT_BOX_FMA_F64 0
 #endif
 #ifndef RT_FLAT_BOX_EXCL_F64  // fp64 flat boxes exclude the face the ray leaves (1) or rely on tmin (0, flat_slab)
 #define RT_FLAT_BOX_EXCL_F64 0  // C2 fp64 34.6 -> 32.7 ms/frame; full-size C1 / C2 parity unchanged (r04e)
@@ -386,7 +392,7 @@ struct DevScene {
   uint32_t n_wnodes, n_wprim_words, wroot, wide_stack, wide_kinds;
   int32_t has_wide;
   uint32_t wide_big;  // primitives at the head of the word stream, tested before the tree
-  const WNodeH* wnodesh;  // the half-precision octant copies (0: none; RT_WIDE_HALF)
+  const WNodeH* wnodesh;  // the fp16 form of the tree (rt_scene.h WNodeH; 0: none)
   // a tree in HBM keeps at most kWideLdsStack stack entries per lane in LDS; deeper entries (rare:
   // every child of every node on a path hit) go to wide_spill[(depth - kWideLdsStack) * spill_lanes + lane]
   uint32_t* wide_spill;
@@ -1229,35 +1235,24 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
       k3 = slab(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, 3u);
     }
   };
-  // RT_WIDE_HALF: the keys of node c from the ray's octant copy (rt_scene.h WNodeH), and its child codes.
+  // RT_WIDE_HALF_F64: the keys of node c from the tree's fp16 form (rt_scene.h WNodeH), and its child codes.
   // A plane's distance is one fma of its fp16 offset (v_fma_mix_f32): h * inv + b, b = (origin - o) *
   // inv per node and axis. b carries two roundings, |b| 2^-23 at most: the near planes take b - e and
-  // the far ones b + e, e = |b| 2^-22 (+ the fp64 ray's widening w), so no box the float node would
-  // enter is culled; the fma's own rounding is relative, covered by box_slack like the float path's.
-  constexpr bool kHalf = !LDSN && RT_WIDE_HALF;
-  [[maybe_unused]] const unsigned char* hbase = nullptr;
-  [[maybe_unused]] uint32_t hoct = 0;  // byte offset of the ray's octant copy
-  // RT_WIDE_HALF=2: one copy (octant 0: lo planes in nr, hi in fr) and the near / far words picked per
-  // axis by v_perm_b32 with a per-ray selector (sel*: 0x07060504 takes the hi word, 0x03020100 the lo)
-  [[maybe_unused]] uint32_t selx = 0, sely = 0, selz = 0;
-  if constexpr (kHalf) {
-    hbase = (const unsigned char*)sc.wnodesh;
-    if constexpr (RT_WIDE_HALF == 2) {
-      selx = (__float_as_uint(inv.x) >> 31) ? 0x07060504u : 0x03020100u;
-      sely = (__float_as_uint(inv.y) >> 31) ? 0x07060504u : 0x03020100u;
-      selz = (__float_as_uint(inv.z) >> 31) ? 0x07060504u : 0x03020100u;
-    } else {
-      const uint32_t oc = (__float_as_uint(inv.x) >> 31) | (__float_as_uint(inv.y) >> 31) << 1 |
-                          (__float_as_uint(inv.z) >> 31) << 2;
-      hoct = oc * sc.n_wnodes * (uint32_t)sizeof(WNodeH);
-    }
-  }
+  // the far ones b + e, e = |b| 2^-22 + the fp64 ray's widening w, so no box the float node would enter
+  // is culled; the fma's own rounding is relative, covered by box_slack like the float path's. The near
+  // and far words of each axis are picked by v_perm_b32 with a per-ray selector (0x07060504: the hi
+  // word, for a negative direction; 0x03020100: the lo word).
+  constexpr bool kHalf = !LDSN && F64 && RT_WIDE_HALF_F64;
+  [[maybe_unused]] const unsigned char* hbase = kHalf ? (const unsigned char*)sc.wnodesh : nullptr;
+  [[maybe_unused]] const uint32_t selx = (__float_as_uint(inv.x) >> 31) ? 0x07060504u : 0x03020100u,
+                                  sely = (__float_as_uint(inv.y) >> 31) ? 0x07060504u : 0x03020100u,
+                                  selz = (__float_as_uint(inv.z) >> 31) ? 0x07060504u : 0x03020100u;
   [[maybe_unused]] auto half_keys = [&](uint32_t c, uint32_t& k0, uint32_t& k1, uint32_t& k2, uint32_t& k3, uint4& cc) {
-    const unsigned char* hp = hbase + (hoct + c * (uint32_t)sizeof(WNodeH));
+    const unsigned char* hp = hbase + c * (uint32_t)sizeof(WNodeH);
     const uint4 h0 = *(const uint4*)hp;
     uint4 h1 = *(const uint4*)(hp + 16), h2 = *(const uint4*)(hp + 32), h3 = *(const uint4*)(hp + 48);
     cc = *(const uint4*)(hp + 64);
-    if constexpr (RT_WIDE_HALF == 2) {  // lo: x h1.xy, y h1.zw, z h2.xy; hi: x h2.zw, y h3.xy, z h3.zw
+    {  // lo: x h1.xy, y h1.zw, z h2.xy; hi: x h2.zw, y h3.xy, z h3.zw -> near in the lo words, far in the hi
       auto pick = [](uint32_t& lo, uint32_t& hi, uint32_t sel) {
         const uint32_t n = __builtin_amdgcn_perm(hi, lo, sel), f = __builtin_amdgcn_perm(lo, hi, sel);
         lo = n;
@@ -1284,7 +1279,7 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
     auto H = [](uint32_t w, bool hi) {
       return (float)__builtin_bit_cast(_Float16, (uint16_t)(hi ? (w >> 16) : (w & 0xFFFFu)));
     };
-    // nr: x h1.x h1.y, y h1.z h1.w, z h2.x h2.y; fr: x h2.z h2.w, y h3.x h3.y, z h3.z h3.w
+    // near: x h1.x h1.y, y h1.z h1.w, z h2.x h2.y; far: x h2.z h2.w, y h3.x h3.y, z h3.z h3.w
     auto key = [&](uint32_t nx, uint32_t ny, uint32_t nz, uint32_t fx, uint32_t fy, uint32_t fz, bool hi,
                    uint32_t slot) {
       const float tn = fmaxf(fmaxf(fmaf(H(nx, hi), inv.x, bnx), fmaf(H(ny, hi), inv.y, bny)),
@@ -1597,11 +1592,16 @@ __device__ __forceinline__ void flat_quad_test(const FlatQuadT<R>& r, int32_t id
     const uint32_t lo = __float_as_uint(tmin);
     in_t = __float_as_uint(th) - lo <= __float_as_uint(tmax) - lo;
     in_ab = max(__float_as_uint(a), __float_as_uint(b)) <= 0x3f800000u;
-  } else {  // the same order tricks on the 64-bit patterns (non-negative doubles order like their bits)
-    const uint64_t lo = (uint64_t)__double_as_longlong(tmin);
-    in_t = (uint64_t)__double_as_longlong(th) - lo <= (uint64_t)__double_as_longlong(tmax) - lo;
+  } else {
+    // fp64 (round 4): two compares each, no 64-bit subtractions or max. Every compare costs ~4.7 SIMD
+    // cycles whatever its width, a 64-bit add or a v_cndmask with an SGPR mask 4: the
+    // order trick on the bit patterns (2 x v_lshl_add_u64 + compare: 12.7; the u64 max: compare + 2
+    // selects + compare, 17.4) costs more than the plain tests (9.4 each). th in [tmin, tmax] with NaN
+    // and -0.0 outside, as before; a, b in [0, 1] on the bit patterns (non-negative doubles order like
+    // their bits; -0.0 and NaN are above 1.0's)
+    in_t = (th >= tmin) & (th <= tmax);
     const uint64_t ua = (uint64_t)__double_as_longlong(a), ub = (uint64_t)__double_as_longlong(b);
-    in_ab = (ua > ub ? ua : ub) <= 0x3FF0000000000000ull;
+    in_ab = (ua <= 0x3FF0000000000000ull) & (ub <= 0x3FF0000000000000ull);
   }
   const uint64_t key = ((uint64_t)(uint32_t)r.inst << 32) | r.e;
   const bool h = in_t & in_ab & (key != xkey);
@@ -1634,18 +1634,22 @@ struct Slab {
 // from it, below tmin = 0.001 unless the ray grazes the face, which is also when the reference's own quad
 // test of that face (quad.h:30-35, no exclusion either) re-hits it; the six selects per box cost ~100 SIMD
 // cycles per segment.
+// RT_FLAT_BOX_FMA_F64: fp64 distances as fma(p, inv, c) with c = -o * inv per ray (one fma per plane
+// instead of a subtraction and a multiply); the hit face is found again with the same operations.
 template <class R>
-__device__ __forceinline__ Slab<R> flat_slab(const FlatBoxT<R>& b, V<R> o, V<R> inv, R tmin, int32_t excl_i,
-                                             uint32_t xf) {
+__device__ __forceinline__ Slab<R> flat_slab(const FlatBoxT<R>& b, V<R> o, V<R> inv, [[maybe_unused]] V<R> c, R tmin,
+                                             int32_t excl_i, uint32_t xf) {
   Slab<R> s;
   const bool left = (sizeof(R) == 4 || RT_FLAT_BOX_EXCL_F64) && excl_i == b.inst;
   const R ninf = -Num<R>::inf();
-  s.t0[0] = (left & (xf == 0)) ? ninf : (b.lo[0] - o.x) * inv.x;
-  s.t1[0] = (left & (xf == 1)) ? ninf : (b.hi[0] - o.x) * inv.x;
-  s.t0[1] = (left & (xf == 2)) ? ninf : (b.lo[1] - o.y) * inv.y;
-  s.t1[1] = (left & (xf == 3)) ? ninf : (b.hi[1] - o.y) * inv.y;
-  s.t0[2] = (left & (xf == 4)) ? ninf : (b.lo[2] - o.z) * inv.z;
-  s.t1[2] = (left & (xf == 5)) ? ninf : (b.hi[2] - o.z) * inv.z;
+  constexpr bool kF = sizeof(R) == 8 && RT_FLAT_BOX_FMA_F64;
+  auto dist = [&](R p, R oa, R ia, R ca) { return kF ? fma(p, ia, ca) : (p - oa) * ia; };
+  s.t0[0] = (left & (xf == 0)) ? ninf : dist(b.lo[0], o.x, inv.x, c.x);
+  s.t1[0] = (left & (xf == 1)) ? ninf : dist(b.hi[0], o.x, inv.x, c.x);
+  s.t0[1] = (left & (xf == 2)) ? ninf : dist(b.lo[1], o.y, inv.y, c.y);
+  s.t1[1] = (left & (xf == 3)) ? ninf : dist(b.hi[1], o.y, inv.y, c.y);
+  s.t0[2] = (left & (xf == 4)) ? ninf : dist(b.lo[2], o.z, inv.z, c.z);
+  s.t1[2] = (left & (xf == 5)) ? ninf : dist(b.hi[2], o.z, inv.z, c.z);
   s.tn = fmax(fmax(fmin(s.t0[0], s.t1[0]), fmin(s.t0[1], s.t1[1])), fmin(s.t0[2], s.t1[2]));
   s.tf = fmin(fmin(fmax(s.t0[0], s.t1[0]), fmax(s.t0[1], s.t1[1])), fmax(s.t0[2], s.t1[2]));
   s.th = s.tn >= tmin ? s.tn : s.tf;
@@ -1666,10 +1670,11 @@ __device__ __forceinline__ void trace_flat(const DevScene<R>& sc, V<R> o, V<R> d
   flat_quads<0>(sc.flatq, n0, 0, o, d, inv, tmin, tmax, best, xkey);
   flat_quads<1>(sc.flatq + n0, n1, (int32_t)n0, o, d, inv, tmin, tmax, best, xkey);
   flat_quads<2>(sc.flatq + n0 + n1, n2, (int32_t)(n0 + n1), o, d, inv, tmin, tmax, best, xkey);
+  const V<R> cneg = (sizeof(R) == 8 && RT_FLAT_BOX_FMA_F64) ? mkv(-o.x * inv.x, -o.y * inv.y, -o.z * inv.z) : o;
 #pragma unroll 1
   for (uint32_t k = 0; k < sc.n_flatb; k++) {
     const FlatBoxT<R> b = ld_scalar(sc.flatb + k);
-    const Slab<R> s = flat_slab(b, o, inv, tmin, excl_i, xf);
+    const Slab<R> s = flat_slab(b, o, inv, cneg, tmin, excl_i, xf);
     const bool h = (s.tn <= s.tf) & (s.th >= tmin) & (s.th <= tmax);
     tmax = h ? s.th : tmax;
     best = h ? (int32_t)(nq + k) : best;
@@ -1689,7 +1694,7 @@ __device__ __forceinline__ void trace_flat(const DevScene<R>& sc, V<R> o, V<R> d
   // the face of the box: the axis whose slab bound is the hit distance (recomputed exactly
   // as in the loop), on the side the ray enters (or leaves, from inside)
   const FlatBoxT<R>& b = fb[(uint32_t)best - nq];
-  const Slab<R> s = flat_slab(b, o, inv, tmin, excl_i, xf);
+  const Slab<R> s = flat_slab(b, o, inv, cneg, tmin, excl_i, xf);
   const bool enter = s.tn >= tmin;
   int k = 2;
   if (enter) {

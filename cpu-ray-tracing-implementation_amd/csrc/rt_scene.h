@@ -206,30 +206,25 @@ struct alignas(16) WNode {
   uint32_t child[4];
   uint32_t pad[4];
 };
-// The half-precision node (round 4, RT_WIDE_HALF) for trees in HBM, in eight copies, one per ray octant.
-// A node visit of the C4 kernel costs one L1 address-path slot per load instruction whatever its width
-// (tools/l1_rates.hip: a random wave64 load costs the same ~39 CU cycles as dword, dwordx2 or dwordx4), so
-// the 7 loads of a WNode visit are what bounds C4; this node is 5. Child boxes are fp16 offsets from the
-// node's origin (its children's smallest lo corner, a float), rounded outward; the octant copy
-// (sign bits of 1/d: x | y << 1 | z << 2) holds each axis's near planes (lo for a positive direction) in
-// nr and far planes in fr, so a child's six distances need no selection:
-//   nr[2a + h], fr[2a + h]: axis a, children 2h (low half) and 2h + 1 (high half)
-//   child[c]: as WNode (an inner node's index within the same copy, or a leaf code)
-// Unused slots hold +inf offsets (no ray direction enters them).
-#ifndef RT_WIDE_HALF_PAD  // 1: WNodeH padded to 128 B, one node per cache line
-#define RT_WIDE_HALF_PAD 0
-#endif
+// The half-precision node (round 4) for trees in HBM, read by the fp64 rays (RT_WIDE_HALF_F64). A node
+// visit of the HBM kernels costs an L1 address-path slot per load instruction whatever its width
+// (tools/l1_rates.hip: a random wave64 load costs the same ~39 CU cycles as dword, dwordx2 or dwordx4);
+// this node is 5 loads where a WNode visit is 7. Child boxes are fp16 offsets from the node's origin (its
+// children's smallest lo corner, a float), rounded outward:
+//   lo[2a + h], hi[2a + h]: axis a, children 2h (low half) and 2h + 1 (high half)
+//   child[c]: as WNode (an inner node's index, or a leaf code)
+// Unused slots hold +inf offsets (no ray direction enters them). Measured on the C4 stand-in: fp64
+// 504.0 -> 480.8 ms/frame; fp32 rays, whose node test is VALU-cheaper, lost (310.3 -> 370.0: the fp16
+// operands and the per-ray near/far selection cost more issue than the two loads save; eight per-octant
+// copies, 373.7; copies padded to one per 128-byte line, 392.5).
 struct alignas(16) WNodeH {
   float ox, oy, oz;
   uint32_t pad;
-  uint32_t nr[6];
-  uint32_t fr[6];
+  uint32_t lo[6];
+  uint32_t hi[6];
   uint32_t child[4];
-#if RT_WIDE_HALF_PAD
-  uint32_t line_pad[12];
-#endif
 };
-static_assert(sizeof(WNodeH) == (RT_WIDE_HALF_PAD ? 128 : 80), "WNodeH is five 16-byte loads");
+static_assert(sizeof(WNodeH) == 80, "WNodeH is five 16-byte loads");
 constexpr uint32_t kWLeaf = 0x80000000u;
 constexpr uint32_t kWCountShift = 25;  // leaf: up to 64 primitives, first word < 2^25
 constexpr uint32_t kWFirstMask = (1u << kWCountShift) - 1u;
@@ -312,7 +307,7 @@ struct SceneHeader {
   uint32_t wide_kinds;   // WK_* bits
   uint32_t has_wide;
   uint32_t wide_big;     // primitives at the head of the word stream tested before the tree (huge boxes)
-  uint32_t has_wnodesh;  // the WNodeH octant copies are present (8 x n_wnodes nodes from off_wnodesh)
+  uint32_t has_wnodesh;  // the WNodeH form of the same tree is present (n_wnodes nodes from off_wnodesh)
   uint64_t off_wnodesh;
 };
 

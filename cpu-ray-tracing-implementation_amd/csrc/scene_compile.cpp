@@ -657,47 +657,34 @@ inline uint16_t half_up(double x) {
   }
   return (uint16_t)hi;
 }
-// The eight octant copies of a wide tree in WNodeH form (rt_scene.h): copy o, node i at o * n + i.
-// The float node's planes are already rounded outward; the offsets from the origin (float minus float:
-// exact in double) are rounded outward again to fp16.
-std::vector<WNodeH> half_octant_nodes(const std::vector<WNode>& wn) {
-  const size_t n = wn.size();
-  std::vector<WNodeH> out(8 * n);
-  for (size_t i = 0; i < n; i++) {
+// A wide tree in WNodeH form (rt_scene.h). The float node's planes are already rounded outward; the
+// offsets from the origin (float minus float: exact in double) are rounded outward again to fp16.
+std::vector<WNodeH> half_nodes(const std::vector<WNode>& wn) {
+  std::vector<WNodeH> out(wn.size());
+  for (size_t i = 0; i < wn.size(); i++) {
     const WNode& w = wn[i];
     const float* lo[3] = {w.lox, w.loy, w.loz};
     const float* hi[3] = {w.hix, w.hiy, w.hiz};
-    float org[3];
+    WNodeH& h = out[i];
+    float* org[3] = {&h.ox, &h.oy, &h.oz};
     for (int a = 0; a < 3; a++) {
       float m = std::numeric_limits<float>::infinity();
       for (int c = 0; c < 4; c++)
         if (std::isfinite(lo[a][c])) m = std::min(m, lo[a][c]);
-      org[a] = std::isfinite(m) ? m : 0.f;
-    }
-    uint16_t qlo[3][4], qhi[3][4];
-    for (int a = 0; a < 3; a++)
+      *org[a] = std::isfinite(m) ? m : 0.f;
+      uint16_t ql[4], qh[4];
       for (int c = 0; c < 4; c++) {
         const bool used = std::isfinite(lo[a][c]) && std::isfinite(hi[a][c]);
-        qlo[a][c] = used ? half_down((double)lo[a][c] - (double)org[a]) : (uint16_t)0x7C00;
-        qhi[a][c] = used ? half_up((double)hi[a][c] - (double)org[a]) : (uint16_t)0x7C00;
+        ql[c] = used ? half_down((double)lo[a][c] - (double)*org[a]) : (uint16_t)0x7C00;
+        qh[c] = used ? half_up((double)hi[a][c] - (double)*org[a]) : (uint16_t)0x7C00;
       }
-    for (int o = 0; o < 8; o++) {
-      WNodeH& h = out[(size_t)o * n + i];
-      h.ox = org[0];
-      h.oy = org[1];
-      h.oz = org[2];
-      h.pad = 0;
-      for (int a = 0; a < 3; a++) {
-        const bool neg = (o >> a) & 1;  // a negative direction on axis a enters through the hi plane
-        const uint16_t* nq = neg ? qhi[a] : qlo[a];
-        const uint16_t* fq = neg ? qlo[a] : qhi[a];
-        for (int k = 0; k < 2; k++) {
-          h.nr[2 * a + k] = (uint32_t)nq[2 * k] | (uint32_t)nq[2 * k + 1] << 16;
-          h.fr[2 * a + k] = (uint32_t)fq[2 * k] | (uint32_t)fq[2 * k + 1] << 16;
-        }
+      for (int k = 0; k < 2; k++) {
+        h.lo[2 * a + k] = (uint32_t)ql[2 * k] | (uint32_t)ql[2 * k + 1] << 16;
+        h.hi[2 * a + k] = (uint32_t)qh[2 * k] | (uint32_t)qh[2 * k + 1] << 16;
       }
-      for (int c = 0; c < 4; c++) h.child[c] = w.child[c];
     }
+    h.pad = 0;
+    for (int c = 0; c < 4; c++) h.child[c] = w.child[c];
   }
   return out;
 }
@@ -1341,7 +1328,7 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
   words.push_back({0.f, 0.f, 0.f, 0.f});
   words64.push_back({0, 0, 0, 0});
   words64.push_back({0, 0, 0, 0});
-  const std::vector<WNodeH> wh = half_octant_nodes(wn);
+  const std::vector<WNodeH> wh = half_nodes(wn);
   {  // the fp64 blob: the same float nodes, the double words
     SceneHeader& h = out->hdr64;
     h.off_wnodes = append(out->blob64, wn);

@@ -351,6 +351,34 @@ __device__ __forceinline__ void body(double& a0, double& a1, double& a2, double&
 #define X(r) asm volatile("v_cvt_f16_f32 %0, %0" : "+v"(f##r));
       X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
 #undef X
+    } else if constexpr (K == 79) {
+#define X(r) asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(f##r) : "v"(fb) : "vcc");
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 80) {
+#define X(r) asm volatile("v_add_co_u32_e32 %0, vcc, %0, %1" : "+v"(f##r) : "v"(fb) : "vcc");
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 81) {
+#define X(r) asm volatile("v_addc_co_u32_e32 %0, vcc, %0, %1, vcc" : "+v"(f##r) : "v"(fb) : "vcc");
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 82) {
+#define X(r) asm volatile("v_sub_co_u32_e32 %0, vcc, %0, %1" : "+v"(f##r) : "v"(fb) : "vcc");
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 83) {
+#define X(r) asm volatile("v_mul_i32_i24 %0, %0, %1" : "+v"(f##r) : "v"(fb) : "vcc");
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 84) {
+#define X(r) asm volatile("v_lshlrev_b16 %0, %0, %1" : "+v"(f##r) : "v"(fb) : "vcc");
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
+    } else if constexpr (K == 85) {
+#define X(r) asm volatile("v_max_i16 %0, %0, %1" : "+v"(f##r) : "v"(fb) : "vcc");
+      X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#undef X
     } else if constexpr (K == 19) {
 #define X(r) { uint64_t t; asm volatile("v_cmp_class_f64_e64 %0, %1, %2" : "=s"(t) : "v"(a##r), "v"(f0)); s##r ^= t; }
       X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
@@ -405,6 +433,7 @@ int main() {
       {"v_ashrrev_i32", k_rate<67>}, {"v_mul_hi_u32_u24", k_rate<68>}, {"v_max_f32", k_rate<69>}, {"v_not_b32", k_rate<70>},
       {"v_cvt_f32_f16", k_rate<71>}, {"v_cvt_u32_f32", k_rate<72>}, {"v_cvt_i32_f32", k_rate<73>}, {"v_fract_f32", k_rate<74>},
       {"v_floor_f32", k_rate<75>}, {"v_trunc_f32", k_rate<76>}, {"v_rndne_f32", k_rate<77>}, {"v_cvt_f16_f32", k_rate<78>},
+      {"v_cndmask_b32_e32", k_rate<79>}, {"v_add_co_u32", k_rate<80>}, {"v_addc_co_u32", k_rate<81>}, {"v_sub_co_u32", k_rate<82>}, {"v_mul_i32_i24", k_rate<83>}, {"v_lshlrev_b16", k_rate<84>}, {"v_max_i16", k_rate<85>},
   };
   int ncu = 0;
   CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
