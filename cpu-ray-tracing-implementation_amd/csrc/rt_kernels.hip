@@ -109,6 +109,12 @@ static double env_f64(const char* name, double dflt) {
 // eighth in items of 8 23.6 / 3.47, with the last quarter 23.7-23.9 / 3.38 (the one-GPU frame, the
 // headline, is kept).
 constexpr uint32_t kMaxItemsPerPixel = 256;
+// items a frame should have at least (render(); RT_ITEMS_TARGET overrides). C1 (400x400, 64 spp), ms/frame
+// by target (item size): fp64 none (16) 0.918, 1 M (8) 0.792, 2.5 M (4) 0.735, 5 M (2) 0.710; fp32 none
+// (32 + tail items of 8) 0.661, 1 M 0.589, 2.5 M 0.525, 5 M 0.536. The BASELINE configs from C2 up have
+// 40 M items or more and keep their sizes.
+constexpr uint32_t kItemsTarget = 4000000;
+constexpr uint32_t kMinAutoChunk = 2;
 static uint32_t auto_chunk(bool flat) {
   return std::max(1u, flat ? env_u32("RT_ITEM_CHUNK_FLAT", 2 * kAutoChunk) : env_u32("RT_ITEM_CHUNK", kAutoChunk / 2));
 }
@@ -1851,8 +1857,17 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     // (fewer item ends, dequeues and partial-sum stores; C2: 23.9 -> 23.5 ms/frame)
     const bool flat_prog = (!f64 || RT_F64_TAIL) && hdr.has_flat && prm->traversal != RT_TRAV_ORDERED &&
                            make_view(cam).mode == RT_CAM_PERSPECTIVE && !(hdr.n_texdata > 0 || hdr.has_cell_noise);
-    const uint32_t chunk0 = prm->samples_per_item > 0 ? std::min<uint32_t>((uint32_t)prm->samples_per_item, spp)
-                                                     : std::min<uint32_t>((f64 && !RT_F64_TAIL) ? kAutoChunk : auto_chunk(flat_prog), spp);
+    uint32_t chunk0 = prm->samples_per_item > 0 ? std::min<uint32_t>((uint32_t)prm->samples_per_item, spp)
+                                               : std::min<uint32_t>((f64 && !RT_F64_TAIL) ? kAutoChunk : auto_chunk(flat_prog), spp);
+    // a small frame (C1: 160,000 px x 64 spp is ~2 items of 16 per resident lane) takes smaller items, so
+    // the lanes that finish early find work while the last items run: the automatic size is halved until
+    // the whole frame has kItemsTarget items (the full image's pixels, not this call's tiles: the layout,
+    // and so the image, is the same for any tiling or rank count)
+    if (prm->samples_per_item <= 0) {
+      const uint64_t target = env_u32("RT_ITEMS_TARGET", kItemsTarget);
+      const uint64_t full = (uint64_t)cam->image_width * (uint64_t)cam->image_height;
+      while (chunk0 > kMinAutoChunk && full * ((spp + chunk0 - 1) / chunk0) < target) chunk0 /= 2;
+    }
     // The frame's last items are short (auto item size only): a lane that takes a long item just
     // before the queue runs dry keeps its wave resident while the others idle, and a small frame
     // (one rank of eight) has few items per lane. The last tail_samples of every pixel come in
