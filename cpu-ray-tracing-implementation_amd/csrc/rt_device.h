@@ -108,6 +108,14 @@ __device__ __forceinline__ double fdiv(double a, double b) {
   const double res = fma(fma(-b, q, a), r, q);  // one residual step: ~correctly rounded
   return __builtin_isfinite(res) ? res : q;     // a/0, inf/b, 0/0 as IEEE
 }
+// a / b where the quotient is finite for every ray that can hit (the fp64 sphere roots' (-b -+ sq) / 2a,
+// 2a = 2|d|^2 > 0): fdiv without its non-finite fallback, a class test and two selects per division
+// (round 4: ~13 of the ~60 SIMD cycles; the same bits whenever the result is finite)
+__device__ __forceinline__ double fdiv_fin(double a, double b) {
+  const double r = frcp(b);
+  const double q = a * r;
+  return fma(fma(-b, q, a), r, q);
+}
 __device__ __forceinline__ double frsq(double x) {  // 1/sqrt(x)
   const double r0 = __builtin_amdgcn_rsq(x);
   const double h = 0.5 * x;
@@ -532,9 +540,10 @@ __device__ __forceinline__ bool sphere_roots(T ox, T oy, T oz, T dx, T dy, T dz,
     T c = (fx * fx + fy * fy + fz * fz) - r * r;
     T disc = b * b - T(4) * a * c;
     if (disc < T(0)) return false;
-    T sq = fsqrt(disc);
-    lo = fdiv(-b - sq, T(2) * a);
-    hi = fdiv(-b + sq, T(2) * a);
+    // disc >= 0 here: the refined sqrt needs only the zero check (fsqrt01), and the roots are finite
+    const T sq = fsqrt01(disc);
+    lo = fdiv_fin(-b - sq, T(2) * a);
+    hi = fdiv_fin(-b + sq, T(2) * a);
   } else {
     T ia = fdiv(T(1), a);
     T bh = -(dx * fx + dy * fy + dz * fz);  // -b/2
