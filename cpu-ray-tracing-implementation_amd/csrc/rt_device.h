@@ -39,20 +39,8 @@ namespace rtd {
 #ifndef RT_WIDE_PREFETCH  // a triangle's words loaded with the record's first word (C4 358.9 -> 357.2 ms)
 #define RT_WIDE_PREFETCH 1
 #endif
-// RT_FLAT_BOX_FMA_F64: fp64 flat boxes with plane distances as fma(p, inv, -o * inv) (flat_slab). Off: it
-// saves 1.5 % (C2 fp64 32.13 -> 31.65 ms/frame) but moves box distances by an ulp and edge decisions with
-// them -- 9 of 364,800 full-size C2 pixels beyond 1e-9 of the oracle instead of 0, row RMSE 2e-16 -> 1e-6
-#ifndef RT_FLAT_BOX_FMA_F64
-#define RT_FLAT_BOX_FMA_F64 0
-#endif
-#ifndef RT_FLAT_BOX_EXCL_F64  // fp64 flat boxes exclude the face the ray leaves (1) or rely on tmin (0, flat_slab)
-#define RT_FLAT_BOX_EXCL_F64 0  // C2 fp64 34.6 -> 32.7 ms/frame; full-size C1 / C2 parity unchanged (r04e)
-#endif
 #ifndef RT_LIGHT_PDF_F64  // fp64 axis-aligned light pdf by one reciprocal (light_pdf_aligned, round 4)
 #define RT_LIGHT_PDF_F64 1
-#endif
-#ifndef RT_LIN_F64_RCP  // fp64 linear programs: aligned quads by the ray's refined reciprocals (round 4)
-#define RT_LIN_F64_RCP 0
 #endif
 #ifndef RT_WIDE_OCTPACK
 #define RT_WIDE_OCTPACK 1
@@ -732,15 +720,9 @@ __device__ __forceinline__ R comp(V<R> v) {
 // alpha = (p - lo) * inv is -0.0 on the quad's Q edge when inv < 0 (a negative edge vector, as
 // box() faces have), which the reference accepts (0 <= -0.0) and the bit order would not: the
 // product is formed as fma(p - lo, inv, +0.0), equal to it except that -0.0 becomes +0.0.
-// RINV (fp64): inv holds the ray's refined reciprocals (flat_inv), and t is (plane - o_A) * inv_A as in the
-// flat program (within an ulp of the division) instead of a refined division per quad
-template <int A, int U, int W, class R, bool RINV = false>
+template <int A, int U, int W, class R>
 __device__ __forceinline__ bool aquad_t(const R* f, V<R> o, V<R> d, V<R> inv, R tmin, R tmax, R& t) {
-  R th;
-  if constexpr (sizeof(R) == 8 && RINV)
-    th = (f[0] - comp<A>(o)) * comp<A>(inv);
-  else
-    th = fdiv_inv(f[0] - comp<A>(o), comp<A>(d), comp<A>(inv));
+  const R th = fdiv_inv(f[0] - comp<A>(o), comp<A>(d), comp<A>(inv));
   if constexpr (sizeof(R) == 4) {
     const R a = __builtin_fmaf((comp<U>(o) + th * comp<U>(d)) - f[1], f[3], 0.0f);
     const R b = __builtin_fmaf((comp<W>(o) + th * comp<W>(d)) - f[2], f[4], 0.0f);
@@ -762,14 +744,13 @@ __device__ __forceinline__ bool aquad_t(const R* f, V<R> o, V<R> d, V<R> inv, R 
 }
 template <class R>
 __device__ __forceinline__ bool lin_quad_t(const LinRec<R>& r, V<R> o, V<R> d, V<R> inv, R tmin, R tmax, R& t) {
-  constexpr bool RI = RT_LIN_F64_RCP != 0;
   switch (r.aux) {
-    case 1: return aquad_t<2, 0, 1, R, RI>(r.f, o, d, inv, tmin, tmax, t);
-    case 2: return aquad_t<1, 0, 2, R, RI>(r.f, o, d, inv, tmin, tmax, t);
-    case 3: return aquad_t<2, 1, 0, R, RI>(r.f, o, d, inv, tmin, tmax, t);
-    case 4: return aquad_t<0, 1, 2, R, RI>(r.f, o, d, inv, tmin, tmax, t);
-    case 5: return aquad_t<1, 2, 0, R, RI>(r.f, o, d, inv, tmin, tmax, t);
-    case 6: return aquad_t<0, 2, 1, R, RI>(r.f, o, d, inv, tmin, tmax, t);
+    case 1: return aquad_t<2, 0, 1>(r.f, o, d, inv, tmin, tmax, t);
+    case 2: return aquad_t<1, 0, 2>(r.f, o, d, inv, tmin, tmax, t);
+    case 3: return aquad_t<2, 1, 0>(r.f, o, d, inv, tmin, tmax, t);
+    case 4: return aquad_t<0, 1, 2>(r.f, o, d, inv, tmin, tmax, t);
+    case 5: return aquad_t<1, 2, 0>(r.f, o, d, inv, tmin, tmax, t);
+    case 6: return aquad_t<0, 2, 1>(r.f, o, d, inv, tmin, tmax, t);
     default: break;
   }
   // general quad: the fields of Quad<R> (quad.h:30-52)
@@ -1509,8 +1490,9 @@ __device__ __forceinline__ void trace_linear(const DevScene<R>& sc, V<R> wo, V<R
   const R tmin = R(0.001);
   R tmax = Num<R>::inf();
   V<R> o = wo, d = wd;
-  // fp32: v_rcp_f32; fp64 (RT_LIN_F64_RCP): the refined reciprocals, once per ray and instance
-  const V<R> winv = (sizeof(R) == 8 && RT_LIN_F64_RCP) ? flat_inv(wd) : rcp3(wd);
+  // fp32: v_rcp_f32 once per ray and instance (fp64 divides per quad: per-ray refined reciprocals were
+  // neutral at 3 waves and cost 24 VGPRs)
+  const V<R> winv = rcp3(wd);
   V<R> inv = winv;
   int32_t cur = -1;
   uint32_t jv = 0;
@@ -1557,7 +1539,7 @@ __device__ __forceinline__ void trace_linear(const DevScene<R>& sc, V<R> wo, V<R
         o = op_in(x, o, true);
         d = op_in(x, d, false);
       }
-      inv = (sizeof(R) == 8 && RT_LIN_F64_RCP) ? flat_inv(d) : rcp3(d);
+      inv = rcp3(d);
     } else if (VOL && ty == E_VOLUME) {
       const Volume<R> vol = ld_uniform(sc.vols, idx);
       h = volume_t<R, true>(sc, vol, wo, wd, d, time, tmin, tmax, keys, bounce, jv, th);
@@ -1566,7 +1548,7 @@ __device__ __forceinline__ void trace_linear(const DevScene<R>& sc, V<R> wo, V<R
       o = wo;
       d = wd;
       // fp64: recomputed rather than kept through the loop (6 registers)
-      inv = (sizeof(R) == 8 && RT_LIN_F64_RCP) ? flat_inv(wd) : winv;
+      inv = winv;
     }
     if (h) {
       tmax = th;
@@ -1639,26 +1621,24 @@ template <class R>
 struct Slab {
   R t0[3], t1[3], tn, tf, th;
 };
-// RT_FLAT_BOX_EXCL_F64 = 0 (fp64): no face exclusion. The face a ray leaves is at distance |t| ~ ulp(o) / |d_k|
-// from it, below tmin = 0.001 unless the ray grazes the face, which is also when the reference's own quad
-// test of that face (quad.h:30-35, no exclusion either) re-hits it; the six selects per box cost ~100 SIMD
-// cycles per segment.
-// RT_FLAT_BOX_FMA_F64: fp64 distances as fma(p, inv, c) with c = -o * inv per ray (one fma per plane
-// instead of a subtraction and a multiply); the hit face is found again with the same operations.
+// fp64: no face exclusion. The face a ray leaves is at distance |t| ~ ulp(o) / |d_k| from it, below
+// tmin = 0.001 unless the ray grazes the face, which is also when the reference's own quad test of that face
+// (quad.h:30-35, no exclusion either) re-hits it; the six selects per box cost ~100 SIMD cycles per segment
+// (C2 fp64 34.6 -> 32.7 ms/frame, parity unchanged). Distances as fma(p, inv, -o * inv) were
+// 1.5 % faster but moved edge decisions (9 of 364,800 C2 pixels beyond 1e-9): not kept.
 template <class R>
-__device__ __forceinline__ Slab<R> flat_slab(const FlatBoxT<R>& b, V<R> o, V<R> inv, [[maybe_unused]] V<R> c, R tmin,
-                                             int32_t excl_i, uint32_t xf) {
+__device__ __forceinline__ Slab<R> flat_slab(const FlatBoxT<R>& b, V<R> o, V<R> inv, R tmin, int32_t excl_i,
+                                             uint32_t xf) {
   Slab<R> s;
-  const bool left = (sizeof(R) == 4 || RT_FLAT_BOX_EXCL_F64) && excl_i == b.inst;
+  const bool left = sizeof(R) == 4 && excl_i == b.inst;
   const R ninf = -Num<R>::inf();
-  constexpr bool kF = sizeof(R) == 8 && RT_FLAT_BOX_FMA_F64;
-  auto dist = [&](R p, R oa, R ia, R ca) { return kF ? fma(p, ia, ca) : (p - oa) * ia; };
-  s.t0[0] = (left & (xf == 0)) ? ninf : dist(b.lo[0], o.x, inv.x, c.x);
-  s.t1[0] = (left & (xf == 1)) ? ninf : dist(b.hi[0], o.x, inv.x, c.x);
-  s.t0[1] = (left & (xf == 2)) ? ninf : dist(b.lo[1], o.y, inv.y, c.y);
-  s.t1[1] = (left & (xf == 3)) ? ninf : dist(b.hi[1], o.y, inv.y, c.y);
-  s.t0[2] = (left & (xf == 4)) ? ninf : dist(b.lo[2], o.z, inv.z, c.z);
-  s.t1[2] = (left & (xf == 5)) ? ninf : dist(b.hi[2], o.z, inv.z, c.z);
+  auto dist = [&](R p, R oa, R ia) { return (p - oa) * ia; };
+  s.t0[0] = (left & (xf == 0)) ? ninf : dist(b.lo[0], o.x, inv.x);
+  s.t1[0] = (left & (xf == 1)) ? ninf : dist(b.hi[0], o.x, inv.x);
+  s.t0[1] = (left & (xf == 2)) ? ninf : dist(b.lo[1], o.y, inv.y);
+  s.t1[1] = (left & (xf == 3)) ? ninf : dist(b.hi[1], o.y, inv.y);
+  s.t0[2] = (left & (xf == 4)) ? ninf : dist(b.lo[2], o.z, inv.z);
+  s.t1[2] = (left & (xf == 5)) ? ninf : dist(b.hi[2], o.z, inv.z);
   s.tn = fmax(fmax(fmin(s.t0[0], s.t1[0]), fmin(s.t0[1], s.t1[1])), fmin(s.t0[2], s.t1[2]));
   s.tf = fmin(fmin(fmax(s.t0[0], s.t1[0]), fmax(s.t0[1], s.t1[1])), fmax(s.t0[2], s.t1[2]));
   s.th = s.tn >= tmin ? s.tn : s.tf;
@@ -1679,11 +1659,10 @@ __device__ __forceinline__ void trace_flat(const DevScene<R>& sc, V<R> o, V<R> d
   flat_quads<0>(sc.flatq, n0, 0, o, d, inv, tmin, tmax, best, xkey);
   flat_quads<1>(sc.flatq + n0, n1, (int32_t)n0, o, d, inv, tmin, tmax, best, xkey);
   flat_quads<2>(sc.flatq + n0 + n1, n2, (int32_t)(n0 + n1), o, d, inv, tmin, tmax, best, xkey);
-  const V<R> cneg = (sizeof(R) == 8 && RT_FLAT_BOX_FMA_F64) ? mkv(-o.x * inv.x, -o.y * inv.y, -o.z * inv.z) : o;
 #pragma unroll 1
   for (uint32_t k = 0; k < sc.n_flatb; k++) {
     const FlatBoxT<R> b = ld_scalar(sc.flatb + k);
-    const Slab<R> s = flat_slab(b, o, inv, cneg, tmin, excl_i, xf);
+    const Slab<R> s = flat_slab(b, o, inv, tmin, excl_i, xf);
     const bool h = (s.tn <= s.tf) & (s.th >= tmin) & (s.th <= tmax);
     tmax = h ? s.th : tmax;
     best = h ? (int32_t)(nq + k) : best;
@@ -1703,7 +1682,7 @@ __device__ __forceinline__ void trace_flat(const DevScene<R>& sc, V<R> o, V<R> d
   // the face of the box: the axis whose slab bound is the hit distance (recomputed exactly
   // as in the loop), on the side the ray enters (or leaves, from inside)
   const FlatBoxT<R>& b = fb[(uint32_t)best - nq];
-  const Slab<R> s = flat_slab(b, o, inv, cneg, tmin, excl_i, xf);
+  const Slab<R> s = flat_slab(b, o, inv, tmin, excl_i, xf);
   const bool enter = s.tn >= tmin;
   int k = 2;
   if (enter) {

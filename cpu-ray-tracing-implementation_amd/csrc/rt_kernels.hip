@@ -114,6 +114,8 @@ constexpr uint32_t kMaxItemsPerPixel = 256;
 // (32 + tail items of 8) 0.661, 1 M 0.589, 2.5 M 0.525, 5 M 0.536. The BASELINE configs from C2 up have
 // 40 M items or more and keep their sizes.
 constexpr uint32_t kItemsTarget = 4000000;
+// item partial sums of one pass at most (render(): a call needing more renders its chunks in passes)
+constexpr uint64_t kPartialBudget = 2ull << 30;
 constexpr uint32_t kMinAutoChunk = 2;
 static uint32_t auto_chunk(bool flat) {
   return std::max(1u, flat ? env_u32("RT_ITEM_CHUNK_FLAT", 2 * kAutoChunk) : env_u32("RT_ITEM_CHUNK", kAutoChunk / 2));
@@ -187,6 +189,9 @@ struct Params {
   // two item sizes: chunks [0, k_bulk) hold `chunk` samples, the later ones (the frame's last
   // items in dequeue order) `tail_chunk` <= chunk samples each
   uint32_t k_bulk, tail_chunk;
+  // the render's chunks come in passes (render(): the partial sums of one pass fit a memory budget): this
+  // launch's items are chunks [chunk0, chunk0 + n_items / npix) of every pixel
+  uint32_t chunk0;
   uint64_t npix_m;  // item / npix = (item * npix_m) >> npix_k for every item < 2^31 (div_magic)
   uint32_t npix_k;
   int32_t max_depth;
@@ -411,11 +416,13 @@ __device__ __forceinline__ uint32_t next_item_dyn(const Params<R>& p) {
 }
 
 // An item's first sample and the end of its sample range: bulk items of p.chunk samples, then tail
-// items of p.tail_chunk (the item layout, render())
+// items of p.tail_chunk (the item layout, render()). `lchunk`: the item's chunk within this pass (item =
+// lchunk * npix + the pixel's index); the layout is decided by the frame's chunk, lchunk + chunk0.
 template <class R>
-__device__ __forceinline__ void item_range(const Params<R>& p, uint32_t item, uint32_t& chunk, uint32_t& first,
+__device__ __forceinline__ void item_range(const Params<R>& p, uint32_t item, uint32_t& lchunk, uint32_t& first,
                                            uint32_t& end) {
-  chunk = (uint32_t)(((uint64_t)item * p.npix_m) >> p.npix_k);
+  lchunk = (uint32_t)(((uint64_t)item * p.npix_m) >> p.npix_k);
+  const uint32_t chunk = lchunk + p.chunk0;
   // fp64 items are uniform (the host never gives them a tail): compiled out, the select costs
   // the fp64 Cornell kernel 10 VGPRs, 3 -> 2 waves per SIMD (C2 f64 5.22 -> 4.08 Gsamples/s)
   const bool bulk = (sizeof(R) == 8 && !RT_F64_TAIL) || chunk < p.k_bulk;
@@ -446,9 +453,9 @@ __device__ __forceinline__ uint32_t send_of(const Params<R>& p, const PS& s) {
 // A new work item for the slot: its pixel and that pixel's RNG key.
 template <class R, class PS>
 __device__ __forceinline__ void begin_item(const Params<R>& p, PS& s, uint32_t item) {
-  uint32_t chunk, first, end;
-  item_range(p, item, chunk, first, end);
-  const uint32_t xy = p.pixmap[item - chunk * p.npix];
+  uint32_t lchunk, first, end;
+  item_range(p, item, lchunk, first, end);
+  const uint32_t xy = p.pixmap[item - lchunk * p.npix];
   s.set_item(item);
   s.set_sample(first);
   s.set_xy(xy);
@@ -1398,22 +1405,35 @@ __global__ __launch_bounds__(kBlock) void k_compact(const void* Dp, int prec, co
 }
 
 // ------------------------------------------------------------------ resolve (camera.h:169-170)
+// A render in passes (render()): pass k adds its chunks to the running sums that the earlier passes left in
+// `out` (first: from 0), in chunk order, and the last pass divides -- the same additions in the same order as
+// one pass over every chunk, so the image does not depend on the pass split.
 template <class R>
 __global__ __launch_bounds__(kBlock) void k_resolve(const R* partial, uint32_t npix, uint32_t nchunks, uint32_t spp,
-                                                    R* out) {
+                                                    R* out, int first, int last) {
   uint32_t px = blockIdx.x * kBlock + threadIdx.x;
   if (px >= npix) return;
   R s0 = 0, s1 = 0, s2 = 0;
+  if (!first) {
+    s0 = out[3ull * px];
+    s1 = out[3ull * px + 1];
+    s2 = out[3ull * px + 2];
+  }
   for (uint32_t c = 0; c < nchunks; c++) {
     const R* q = partial + 3ull * ((uint64_t)c * npix + px);
     s0 += q[0];
     s1 += q[1];
     s2 += q[2];
   }
-  R inv = R(spp);
-  out[3ull * px] = s0 / inv;
-  out[3ull * px + 1] = s1 / inv;
-  out[3ull * px + 2] = s2 / inv;
+  if (last) {
+    R inv = R(spp);
+    s0 = s0 / inv;
+    s1 = s1 / inv;
+    s2 = s2 / inv;
+  }
+  out[3ull * px] = s0;
+  out[3ull * px + 1] = s1;
+  out[3ull * px + 2] = s2;
 }
 
 template <class R>
@@ -1744,66 +1764,81 @@ void launch_k(const Params<R>& p, uint32_t grid, hipStream_t st) {
   }
 }
 
-// RT_DEV_ONLY (development builds for register/spill iteration, scripts/kernel_usage.py): instantiate
-// one kernel family only -- 1 the flat program, 2 the wide BVH, 3 the linear programs. 0: everything.
+// The kernel family a render takes, decided on the host from the compiled scene, the camera model, the
+// schedule and the traversal order (launch_step launches it).
+enum KernelFamily { KF_FLAT, KF_LIN_QUAD, KF_LIN_VOL, KF_LIN_SPH, KF_LIN_ALL, KF_WIDE, KF_STACK };
+KernelFamily kernel_family(const SceneHeader& h, int32_t cam_mode, bool persist, bool ordered) {
+  const bool persp = cam_mode == RT_CAM_PERSPECTIVE, procedural = h.n_texdata > 0 || h.has_cell_noise;
+  const bool sph = h.n_spheres > 0, tri = h.n_tris > 0, vol = h.has_volumes != 0;
+  // the flat program (world-space quads and boxes, fp32 and fp64); the extended kernels keep the linear one
+  if (!ordered && h.has_flat && persp && !procedural) return KF_FLAT;
+  if (h.n_linear > 0) {
+    if (!sph && !tri) return vol ? KF_LIN_VOL : KF_LIN_QUAD;
+    return (sph && !tri && !vol) ? KF_LIN_SPH : KF_LIN_ALL;
+  }
+  // the wide BVH (persistent schedule, base kernels; fp64 rays since round 3)
+  if (!ordered && h.has_wide && persist && persp && !procedural) return KF_WIDE;
+  return KF_STACK;
+}
+const char* family_name(KernelFamily f) {
+  static const char* n[] = {"flat program", "linear program (quads)", "linear program (quads + volumes)",
+                            "linear program (spheres)", "linear program (all kinds)", "wide BVH", "binary BVH"};
+  return n[f];
+}
+// RT_DEV_ONLY (development builds for register/spill iteration, scripts/kernel_usage.py): instantiate one
+// kernel family only -- 1 the flat program, 2 the wide BVH, 3 the quad + volume linear program. 0:
+// everything. A render (and rt_scene_check) that needs a family such a build omits fails with
+// RT_ERR_UNSUPPORTED instead of launching nothing.
 #ifndef RT_DEV_ONLY
 #define RT_DEV_ONLY 0
 #endif
+constexpr bool family_built(KernelFamily f) {
+  return RT_DEV_ONLY == 0 || (RT_DEV_ONLY == 1 && f == KF_FLAT) || (RT_DEV_ONLY == 2 && f == KF_WIDE) ||
+         (RT_DEV_ONLY == 3 && f == KF_LIN_VOL);
+}
 template <class R>
-void launch_step(const Params<R>& p, int stack, bool sph, bool tri, uint32_t grid, hipStream_t st) {
-#if RT_DEV_ONLY == 1
-  if (RT_FLAT_LDS && p.persist && FlatTrav<R, true>::tables_fit(p.sc))
-    launch_k<R, FlatTrav<R, true>>(p, grid, st);
-  else
-    launch_k<R, FlatTrav<R>>(p, grid, st);
-  return;
-#elif RT_DEV_ONLY == 2
-  launch_wide(p, grid, st);
-  return;
-#elif RT_DEV_ONLY == 3
-  launch_k<R, LinearTrav<R, false, false, true>>(p, grid, st);
-  return;
-#else
-  const bool vol = p.sc.has_volumes != 0;
-  // the flat program (world-space quads and boxes, fp32 and fp64); the extended kernels keep the linear one
-  if (p.sc.has_flat && p.cam_mode == RT_CAM_PERSPECTIVE && !p.sc.has_procedural) {
-    if (RT_FLAT_LDS && p.persist && FlatTrav<R, true>::tables_fit(p.sc))
-      launch_k<R, FlatTrav<R, true>>(p, grid, st);
-    else
-      launch_k<R, FlatTrav<R>>(p, grid, st);
-    return;
+void launch_step(const Params<R>& p, KernelFamily fam, int stack, uint32_t grid, hipStream_t st) {
+  switch (fam) {
+    case KF_FLAT:
+      if constexpr (family_built(KF_FLAT)) {
+        if (RT_FLAT_LDS && p.persist && FlatTrav<R, true>::tables_fit(p.sc))
+          launch_k<R, FlatTrav<R, true>>(p, grid, st);
+        else
+          launch_k<R, FlatTrav<R>>(p, grid, st);
+      }
+      return;
+    case KF_LIN_QUAD:
+      if constexpr (family_built(KF_LIN_QUAD)) launch_k<R, LinearTrav<R, false, false, false>>(p, grid, st);
+      return;
+    case KF_LIN_VOL:
+      if constexpr (family_built(KF_LIN_VOL)) launch_k<R, LinearTrav<R, false, false, true>>(p, grid, st);
+      return;
+    case KF_LIN_SPH:
+      if constexpr (family_built(KF_LIN_SPH)) launch_k<R, LinearTrav<R, true, false, false>>(p, grid, st);
+      return;
+    case KF_LIN_ALL:
+      if constexpr (family_built(KF_LIN_ALL)) launch_k<R, LinearTrav<R, true, true, true>>(p, grid, st);
+      return;
+    case KF_WIDE:
+      if constexpr (family_built(KF_WIDE)) launch_wide(p, grid, st);
+      return;
+    case KF_STACK:
+      if constexpr (family_built(KF_STACK)) {
+        if constexpr (sizeof(R) == 4) {  // nodes in LDS: fp32 only
+          if (p.sc.n_nodes <= kLdsNodeMax && stack <= 16) {
+            launch_k<R, StackTrav<R, 16, true>>(p, grid, st);
+            return;
+          }
+        }
+        if (stack <= 8)
+          launch_k<R, StackTrav<R, 8>>(p, grid, st);
+        else if (stack <= 16)
+          launch_k<R, StackTrav<R, 16>>(p, grid, st);
+        else
+          launch_k<R, StackTrav<R, kStackDepth>>(p, grid, st);
+      }
+      return;
   }
-  if (p.sc.n_linear > 0) {
-    if (!sph && !tri && !vol)
-      launch_k<R, LinearTrav<R, false, false, false>>(p, grid, st);
-    else if (!sph && !tri && vol)
-      launch_k<R, LinearTrav<R, false, false, true>>(p, grid, st);
-    else if (sph && !tri && !vol)
-      launch_k<R, LinearTrav<R, true, false, false>>(p, grid, st);
-    else
-      launch_k<R, LinearTrav<R, true, true, true>>(p, grid, st);
-  } else if (p.sc.has_wide && p.persist && p.cam_mode == RT_CAM_PERSPECTIVE && !p.sc.has_procedural) {
-    launch_wide(p, grid, st);  // the wide BVH (persistent schedule, base kernels; fp64 rays since round 3)
-  } else if constexpr (sizeof(R) == 4) {
-    if (p.sc.n_nodes <= kLdsNodeMax && stack <= 16) {
-      launch_k<R, StackTrav<R, 16, true>>(p, grid, st);
-    } else if (stack <= 8) {
-      launch_k<R, StackTrav<R, 8>>(p, grid, st);
-    } else if (stack <= 16) {
-      launch_k<R, StackTrav<R, 16>>(p, grid, st);
-    } else {
-      launch_k<R, StackTrav<R, kStackDepth>>(p, grid, st);
-    }
-  } else if (sizeof(R) == 4 && p.sc.n_nodes <= kLdsNodeMax && stack <= 16) {
-    launch_k<R, StackTrav<R, 16, true>>(p, grid, st);
-  } else if (stack <= 8) {
-    launch_k<R, StackTrav<R, 8>>(p, grid, st);
-  } else if (stack <= 16) {
-    launch_k<R, StackTrav<R, 16>>(p, grid, st);
-  } else {
-    launch_k<R, StackTrav<R, kStackDepth>>(p, grid, st);
-  }
-#endif
 }
 
 template <class R>
@@ -1886,12 +1921,21 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
         tail_chunk = std::min(chunk, 2 * tail_chunk);
       }
     }
-    const uint64_t n_items64 = (uint64_t)npix * nchunks;
-    if (n_items64 >= (1ull << 31)) return set_err(c, RT_ERR_INVALID_ARGUMENT, "too many work items in one call");
-    const uint32_t n_items = (uint32_t)n_items64;
+    // Passes: the item partial sums of a call are 3 R per (pixel, chunk) -- C5 fp64 (3840 x 2160 at 4096 spp,
+    // 192 chunks) would need 38 GB. The chunks come in passes of `cpp` chunks whose partial sums fit
+    // kPartialBudget (and whose items fit 32 bits); every pass is one launch, and its resolve adds its chunks
+    // to the running per-pixel sums in chunk order (k_resolve), so the image is the same for any split.
+    const uint64_t budget = (uint64_t)env_f64("RT_PARTIAL_BUDGET", (double)kPartialBudget);
+    const uint64_t per_chunk = 3ull * sizeof(R) * npix;
+    const uint32_t cpp = (uint32_t)std::max<uint64_t>(
+        1, std::min<uint64_t>({(uint64_t)nchunks, budget / per_chunk, ((1ull << 31) - 1) / npix}));
+    const uint32_t n_items = npix * cpp;  // items of the largest pass
     // the default schedule is persistent (k_persist); an explicit segments_per_launch selects the
     // launch-per-K-segments wavefront with HBM path state and live-slot compaction
     const bool persist = prm->segments_per_launch <= 0;
+    const KernelFamily fam = kernel_family(hdr, cam->mode, persist, prm->traversal == RT_TRAV_ORDERED);
+    if (!family_built(fam))
+      return set_err(c, RT_ERR_UNSUPPORTED, std::string("this build (RT_DEV_ONLY) has no ") + family_name(fam) + " kernels");
     uint32_t P = prm->pool_slots > 0 ? (uint32_t)prm->pool_slots
                  : persist       ? kAutoPersistLanes
                                  : (f64 ? kAutoPool64 : kAutoPool32);
@@ -1907,6 +1951,8 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
       if ((s = ensure(c, c->queue1, 4ull * P)) != RT_OK) return s;
     }
     if ((s = ensure(c, c->partial, 3ull * n_items * sizeof(R))) != RT_OK) return s;
+    c->last.passes += (nchunks + cpp - 1) / cpp;
+    c->last.partial_bytes = 3ull * n_items * sizeof(R);
     const size_t pixmap_bytes = c->pixmap.bytes;
     if ((s = ensure(c, c->pixmap, 4ull * npix)) != RT_OK) return s;
     if (c->pixmap.bytes != pixmap_bytes) c->tiles_dev.clear();  // reallocated: the old map is gone
@@ -1978,84 +2024,93 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     if (c->timing && c->ev_used > 4096 && (s = settle(c)) != RT_OK) return s;  // bound the pending events
     const size_t ev0 = c->ev_used;
     if (persist) {
-      // one launch of P lanes (pool_slots, or kAutoPersistLanes)
       if ((s = ensure(c, c->fault, 4)) != RT_OK) return s;
       p.persist = RT_PERSIST_MODE;
       p.fault = (uint32_t*)c->fault.ptr;
       if ((s = ensure(c, c->heads, 4ull * kHeads * kHeadStride)) != RT_OK) return s;
-      RT_HIP(c, hipMemsetAsync(c->heads.ptr, 0, 4ull * kHeads * kHeadStride, st));
       p.heads = (uint32_t*)c->heads.ptr;
-      const uint32_t grid = nblk_max;
-      hipEvent_t e0 = nullptr, e1 = nullptr;
-      if (c->timing) {
-        e0 = take_event(c, ev0);
-        e1 = take_event(c, ev0 + 1);
-        if (!e0 || !e1) return set_err(c, RT_ERR_HIP, "hipEventCreate failed");
-        RT_HIP(c, hipEventRecord(e0, st));
-      }
-      launch_step<R>(p, cs.stack_need, hdr.n_spheres > 0, hdr.n_tris > 0, grid, st);
-      RT_HIP(c, hipGetLastError());
-      c->last.grid_lanes = t_grid_lanes;
-      if (c->timing) {
-        RT_HIP(c, hipEventRecord(e1, st));
-        ev = 2;
-      }
-      launches = iters = 1;
-      // a fault is reported by the settle after this call (rt_stats, or a host-output render)
-    } else {
-    if (p.cam_mode != RT_CAM_PERSPECTIVE || p.sc.has_procedural)
-      hipLaunchKernelGGL((k_init<R, true>), dim3(nblk_max), dim3(kBlock), 0, st, p);
-    else
-      hipLaunchKernelGGL((k_init<R, false>), dim3(nblk_max), dim3(kBlock), 0, st, p);
-    launches = 1;
-    uint32_t* qbuf[2] = {(uint32_t*)c->queue0.ptr, (uint32_t*)c->queue1.ptr};
-    int qsel = 0;
-    uint32_t* blk = (uint32_t*)c->blk.ptr;
-    uint32_t* d_total = blk + nblk_max + 1;
-    // every slot finishes within (items per slot) * chunk * max_depth segments; anything longer is a bug
-    const uint64_t iter_cap =
-        (((uint64_t)(n_items + P - 1) / P) * chunk * (uint64_t)prm->max_depth + K - 1) / K + 4 * kBatch;
-    for (;;) {
-      if (iters > iter_cap) return set_err(c, RT_ERR_HIP, "wavefront did not drain (internal error)");
-      const uint32_t grid = (p.n + kBlock - 1) / kBlock;
-      for (int b = 0; b < kBatch; b++) {
+    }
+    for (uint32_t c0 = 0; c0 < nchunks; c0 += cpp) {  // the passes (one for every BASELINE config but C5)
+      const uint32_t pc = std::min(cpp, nchunks - c0);
+      p.chunk0 = c0;
+      p.n_items = npix * pc;
+      if (persist) {
+        // one launch of P lanes (pool_slots, or kAutoPersistLanes)
+        RT_HIP(c, hipMemsetAsync(c->heads.ptr, 0, 4ull * kHeads * kHeadStride, st));
+        const uint32_t grid = nblk_max;
         if (c->timing) {
           hipEvent_t e0 = take_event(c, ev0 + ev), e1 = take_event(c, ev0 + ev + 1);
           if (!e0 || !e1) return set_err(c, RT_ERR_HIP, "hipEventCreate failed");
           RT_HIP(c, hipEventRecord(e0, st));
-          launch_step<R>(p, cs.stack_need, hdr.n_spheres > 0, hdr.n_tris > 0, grid, st);
+          launch_step<R>(p, fam, cs.stack_need, grid, st);
           RT_HIP(c, hipEventRecord(e1, st));
           ev += 2;
         } else {
-          launch_step<R>(p, cs.stack_need, hdr.n_spheres > 0, hdr.n_tris > 0, grid, st);
+          launch_step<R>(p, fam, cs.stack_need, grid, st);
         }
+        RT_HIP(c, hipGetLastError());
+        c->last.grid_lanes = t_grid_lanes;
         launches++;
         iters++;
-      }
-      RT_HIP(c, hipGetLastError());
-      // live-slot count; compact into a queue once half the pool has finished
-      hipLaunchKernelGGL(k_count, dim3(grid), dim3(kBlock), 0, st, (const void*)p.D, (int)f64, p.queue, p.n, blk);
-      hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, blk, grid, d_total);
-      launches += 2;
-      RT_HIP(c, hipMemcpyAsync(c->total_host, d_total, 4, hipMemcpyDeviceToHost, st));
-      RT_HIP(c, hipStreamSynchronize(st));
-      uint32_t alive = *c->total_host;
-      if (alive == 0) break;
-      if (p.queue || alive * 2 <= p.P) {
-        uint32_t* nq = qbuf[qsel];
-        qsel ^= 1;
-        hipLaunchKernelGGL(k_compact, dim3(grid), dim3(kBlock), 0, st, (const void*)p.D, (int)f64, p.queue, p.n,
-                           (const uint32_t*)blk, nq);
+        // a fault is reported by the settle after this call (rt_stats, or a host-output render)
+      } else {
+        p.queue = nullptr;
+        p.n = P;
+        if (p.cam_mode != RT_CAM_PERSPECTIVE || p.sc.has_procedural)
+          hipLaunchKernelGGL((k_init<R, true>), dim3(nblk_max), dim3(kBlock), 0, st, p);
+        else
+          hipLaunchKernelGGL((k_init<R, false>), dim3(nblk_max), dim3(kBlock), 0, st, p);
         launches++;
-        p.queue = nq;
-        p.n = alive;
+        uint32_t* qbuf[2] = {(uint32_t*)c->queue0.ptr, (uint32_t*)c->queue1.ptr};
+        int qsel = 0;
+        uint32_t* blk = (uint32_t*)c->blk.ptr;
+        uint32_t* d_total = blk + nblk_max + 1;
+        // every slot finishes within (items per slot) * chunk * max_depth segments; anything longer is a bug
+        const uint64_t iter_cap =
+            iters + (((uint64_t)(p.n_items + P - 1) / P) * chunk * (uint64_t)prm->max_depth + K - 1) / K + 4 * kBatch;
+        for (;;) {
+          if (iters > iter_cap) return set_err(c, RT_ERR_HIP, "wavefront did not drain (internal error)");
+          const uint32_t grid = (p.n + kBlock - 1) / kBlock;
+          for (int b = 0; b < kBatch; b++) {
+            if (c->timing) {
+              hipEvent_t e0 = take_event(c, ev0 + ev), e1 = take_event(c, ev0 + ev + 1);
+              if (!e0 || !e1) return set_err(c, RT_ERR_HIP, "hipEventCreate failed");
+              RT_HIP(c, hipEventRecord(e0, st));
+              launch_step<R>(p, fam, cs.stack_need, grid, st);
+              RT_HIP(c, hipEventRecord(e1, st));
+              ev += 2;
+            } else {
+              launch_step<R>(p, fam, cs.stack_need, grid, st);
+            }
+            launches++;
+            iters++;
+          }
+          RT_HIP(c, hipGetLastError());
+          // live-slot count; compact into a queue once half the pool has finished
+          hipLaunchKernelGGL(k_count, dim3(grid), dim3(kBlock), 0, st, (const void*)p.D, (int)f64, p.queue, p.n, blk);
+          hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, blk, grid, d_total);
+          launches += 2;
+          RT_HIP(c, hipMemcpyAsync(c->total_host, d_total, 4, hipMemcpyDeviceToHost, st));
+          RT_HIP(c, hipStreamSynchronize(st));
+          uint32_t alive = *c->total_host;
+          if (alive == 0) break;
+          if (p.queue || alive * 2 <= p.P) {
+            uint32_t* nq = qbuf[qsel];
+            qsel ^= 1;
+            hipLaunchKernelGGL(k_compact, dim3(grid), dim3(kBlock), 0, st, (const void*)p.D, (int)f64, p.queue, p.n,
+                               (const uint32_t*)blk, nq);
+            launches++;
+            p.queue = nq;
+            p.n = alive;
+          }
+        }
       }
+      hipLaunchKernelGGL(k_resolve<R>, dim3((npix + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
+                         (const R*)c->partial.ptr, npix, pc, spp, (R*)dout, (int)(c0 == 0),
+                         (int)(c0 + pc >= nchunks));
+      launches++;
+      RT_HIP(c, hipGetLastError());
     }
-    }  // !persist
-    hipLaunchKernelGGL(k_resolve<R>, dim3((npix + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
-                       (const R*)c->partial.ptr, npix, nchunks, spp, (R*)dout);
-    launches++;
-    RT_HIP(c, hipGetLastError());
     // device output: nothing waits here -- the segment counters (cumulative on the device), the
     // timing events and the fault word are settled by rt_stats, rt_reset_counters or a host-output call
     c->ev_used = ev0 + ev;
@@ -2178,6 +2233,13 @@ rt_status rt_scene_check(const rt_scene_desc* desc, rt_scene_info* info, char* e
   std::string m;
   rt_status s = desc ? compile_scene(desc, &cs, &m) : RT_ERR_INVALID_ARGUMENT;
   if (!desc) m = "null descriptor";
+  if (s == RT_OK) {  // the kernels a perspective render on the default (persistent) schedule would take
+    const KernelFamily fam = kernel_family(cs.hdr, RT_CAM_PERSPECTIVE, true, false);
+    if (!family_built(fam)) {
+      s = RT_ERR_UNSUPPORTED;
+      m = std::string("this build (RT_DEV_ONLY) has no ") + family_name(fam) + " kernels";
+    }
+  }
   if (err && errlen > 0) std::snprintf(err, (size_t)errlen, "%s", m.c_str());
   if (s == RT_OK && info) {
     const SceneHeader& h = cs.hdr;

@@ -674,8 +674,13 @@ std::vector<WNodeH> half_nodes(const std::vector<WNode>& wn) {
       *org[a] = std::isfinite(m) ? m : 0.f;
       uint16_t ql[4], qh[4];
       for (int c = 0; c < 4; c++) {
-        const bool used = std::isfinite(lo[a][c]) && std::isfinite(hi[a][c]);
-        ql[c] = used ? half_down((double)lo[a][c] - (double)*org[a]) : (uint16_t)0x7C00;
+        // unused slots are exactly the builder's sentinel lo = +inf; a used child whose float plane saturated
+        // (a box beyond float range: down() / up() give -inf / +inf) keeps an infinite offset on that side
+        // (fp16 -inf = 0xFC00 below the origin, half_up(+inf) = +inf above it), so fp64 rays cull it no more
+        // than the float node does
+        const bool used = !(lo[a][c] == std::numeric_limits<float>::infinity());
+        const bool lo_inf = lo[a][c] == -std::numeric_limits<float>::infinity();
+        ql[c] = !used ? (uint16_t)0x7C00 : lo_inf ? (uint16_t)0xFC00 : half_down((double)lo[a][c] - (double)*org[a]);
         qh[c] = used ? half_up((double)hi[a][c] - (double)*org[a]) : (uint16_t)0x7C00;
       }
       for (int k = 0; k < 2; k++) {
@@ -1321,6 +1326,12 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
     std::fprintf(stderr, "[wide] ok %d need %d nodes %zu words %zu binary nodes %zu\n", (int)ok, need, wn.size(),
                  words.size(), bn.size());
   if (!ok || need > kWideStackMax) return false;
+  // the HBM kernels address nodes and primitive words by 32-bit byte offsets from the tree's base (fp32
+  // rays: node * sizeof(WNode), word * 16; fp64 rays: node * sizeof(WNodeH), word * 32): a tree past 4 GiB
+  // (~40 M nodes) takes the binary BVH instead
+  if ((uint64_t)wn.size() * std::max(sizeof(WNode), sizeof(WNodeH)) >= (1ull << 32) ||
+      ((uint64_t)words.size() + 2) * 32u >= (1ull << 32))
+    return false;
 
   // two zero words past the last record: kernels with triangles read a record's next two words with
   // its first (trace_wide test_prims), past the end for a trailing sphere
@@ -1347,8 +1358,7 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
   }
   SceneHeader& h = out->hdr;
   h.off_wnodes = append(out->blob32, wn);
-  h.off_wnodesh = append(out->blob32, wh);
-  h.has_wnodesh = 1;
+  h.has_wnodesh = 0;  // only fp64 rays read the fp16 form (RT_WIDE_HALF_F64): it stays out of the fp32 blob
   h.off_wprims = append(out->blob32, words);
   out->blob32.resize((out->blob32.size() + 255) & ~size_t(255));
   h.bytes = out->blob32.size();

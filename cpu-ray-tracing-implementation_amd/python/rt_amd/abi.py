@@ -26,7 +26,7 @@ RT_TEX_SOLID, RT_TEX_CHECKER, RT_TEX_PERLIN, RT_TEX_VALUE, RT_TEX_WORLEY, RT_TEX
 RT_CAM_PERSPECTIVE, RT_CAM_ORTHONORMAL, RT_CAM_FISHEYE, RT_CAM_LENS = range(4)
 RT_PREC_F32, RT_PREC_F64 = 0, 1
 RT_TRAV_AUTO, RT_TRAV_ORDERED = 0, 1
-ABI_VERSION = 7  # include/rt_hip.h RT_ABI_VERSION
+ABI_VERSION = 8  # include/rt_hip.h RT_ABI_VERSION
 
 
 class rt_object(ctypes.Structure):
@@ -74,7 +74,7 @@ class rt_tile(ctypes.Structure):
 class rt_counters(ctypes.Structure):
     _fields_ = [("segments", c_uint64), ("samples", c_uint64), ("iterations", c_uint64), ("launches", c_uint64),
                 ("last_render_ms", c_double), ("step_ms", c_double), ("aux_ms", c_double),
-                ("grid_lanes", c_uint64)]
+                ("grid_lanes", c_uint64), ("passes", c_uint64), ("partial_bytes", c_uint64)]
 
 
 class rt_scene_info(ctypes.Structure):

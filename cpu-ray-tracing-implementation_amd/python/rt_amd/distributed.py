@@ -34,11 +34,25 @@ class FrameSharding:
         return out, fb
 
     def frame(self, ctx, cam, params, out, fb, stream=None):
-        """Render this rank's tiles into `out` (queued on `stream`, default torch's current stream),
-        gather every rank's buffer to rank 0 and scatter them into `fb` (rank 0)."""
+        """Render this rank's tiles into `out`, gather every rank's buffer to rank 0 and scatter them into
+        `fb` (rank 0). The render is queued on `stream` (a torch.cuda.Stream; default torch's current
+        stream). The gather and the scatter are ordered against torch's current stream, so a render on
+        another stream is joined to it by an event first."""
         if stream is None:
-            stream = torch.cuda.current_stream(self.device).cuda_stream
-        ctx.render_tiles(cam, params, self.my_tiles, out.data_ptr(), 1, stream)
+            handle = torch.cuda.current_stream(self.device).cuda_stream
+            ctx.render_tiles(cam, params, self.my_tiles, out.data_ptr(), 1, handle)
+        elif isinstance(stream, torch.cuda.Stream):
+            ctx.render_tiles(cam, params, self.my_tiles, out.data_ptr(), 1, stream.cuda_stream)
+            cur = torch.cuda.current_stream(self.device)
+            if stream != cur:
+                ev = torch.cuda.Event()
+                ev.record(stream)
+                cur.wait_event(ev)
+        else:  # a raw handle: only the current stream's (or 0 for a CPU rehearsal without a GPU) is ordered
+            if torch.cuda.is_available() and stream not in (0, torch.cuda.current_stream(self.device).cuda_stream):
+                raise ValueError("pass a torch.cuda.Stream: a raw handle of another stream cannot be ordered "
+                                 "before the gather")
+            ctx.render_tiles(cam, params, self.my_tiles, out.data_ptr(), 1, stream)
         if self.world == 1:
             parts = [out]
         elif self.backend == "gloo":  # host-memory gather (the device buffer is copied behind the render)

@@ -65,6 +65,8 @@ inline bool decode(const std::vector<uint8_t>& d, Image& im, std::string* err) {
   if (std::strncmp(s, "+X ", 3) != 0) return fail("HDR: unsupported data layout");
   const long w = std::strtol(s + 3, nullptr, 10);
   if (w <= 0 || h <= 0 || w > (1 << 24) || h > (1 << 24)) return fail("HDR: bad size");
+  // stbi__mad4sizes_valid(w, h, 3, sizeof(float)): refused before anything is allocated
+  if ((uint64_t)w * (uint64_t)h * 3u * sizeof(float) > 0x7FFFFFFFull) return fail("HDR: image too large");
   im.width = (int)w;
   im.height = (int)h;
   im.rgb.assign((size_t)w * h * 3, 0.0f);

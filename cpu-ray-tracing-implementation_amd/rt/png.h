@@ -86,7 +86,11 @@ struct Huff {
   }
 };
 
-inline bool inflate(const uint8_t* in, size_t n, std::vector<uint8_t>& out, std::string* err) {
+// `limit`: stop once this many bytes are out (the image's filtered size: a crafted stream cannot grow the
+// buffer past what the header's dimensions use; stb keeps decoding and ignores the surplus, so the pixels
+// are the same)
+inline bool inflate(const uint8_t* in, size_t n, std::vector<uint8_t>& out, std::string* err,
+                    size_t limit = ~size_t(0)) {
   static const uint16_t lbase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
                                      31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
   static const uint8_t lext[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
@@ -105,6 +109,7 @@ inline bool inflate(const uint8_t* in, size_t n, std::vector<uint8_t>& out, std:
       const uint32_t len = b.get(16), nlen = b.get(16);
       if ((len ^ 0xFFFFu) != nlen) return fail("zlib: stored block length");
       for (uint32_t i = 0; i < len; i++) out.push_back((uint8_t)b.get(8));
+      if (out.size() >= limit) return true;
     } else if (type == 1 || type == 2) {
       Huff lit, dist;
       uint8_t lens[320];
@@ -151,6 +156,7 @@ inline bool inflate(const uint8_t* in, size_t n, std::vector<uint8_t>& out, std:
         if (s < 0) return fail("zlib: bad literal/length code");
         if (s < 256) {
           out.push_back((uint8_t)s);
+          if (out.size() >= limit) return true;
         } else if (s == 256) {
           break;
         } else {
@@ -163,6 +169,7 @@ inline bool inflate(const uint8_t* in, size_t n, std::vector<uint8_t>& out, std:
           if (d > out.size()) return fail("zlib: distance too far back");
           const size_t from = out.size() - d;
           for (size_t i = 0; i < len; i++) out.push_back(out[from + i]);
+          if (out.size() >= limit) return true;
         }
         if (b.bad) return fail("zlib: truncated");
       }
@@ -241,8 +248,25 @@ inline bool decode(const std::vector<uint8_t>& d, Image& im, std::string* err) {
   if (ctype == 3 && pal.size() < 3) return fail("PNG: palette missing");
   if (idat.size() < 2 || (idat[0] & 15) != 8 || ((idat[0] << 8) | idat[1]) % 31 != 0 || (idat[1] & 32))
     return fail("PNG: bad zlib header");
+  // stb_image.h:5124-5129 ("Image too large to decode"): refused before anything is allocated
+  if ((1u << 30) / w / (uint32_t)(ctype == 3 ? 4 : ch) < h) return fail("PNG: image too large");
+  // the filtered size the header implies (every pass's rows, a filter byte each): inflate stops there,
+  // and fewer bytes than that is a corrupt image (stb: "not enough pixels") -- checked before the
+  // output is allocated
+  auto pass_bytes = [&](uint32_t x0, uint32_t y0, uint32_t dx, uint32_t dy) -> uint64_t {
+    const uint64_t pw = x0 < w ? (w - x0 + dx - 1) / dx : 0, ph = y0 < h ? (h - y0 + dy - 1) / dy : 0;
+    return pw == 0 || ph == 0 ? 0 : ((pw * ch * depth + 7) / 8 + 1) * ph;
+  };
+  static const uint32_t ax[7] = {0, 4, 0, 2, 0, 1, 0}, ay[7] = {0, 0, 4, 0, 2, 0, 1};
+  static const uint32_t adx[7] = {8, 8, 4, 4, 2, 2, 1}, ady[7] = {8, 8, 8, 4, 4, 2, 2};
+  uint64_t expect = 0;
+  if (!interlace)
+    expect = pass_bytes(0, 0, 1, 1);
+  else
+    for (int k = 0; k < 7; k++) expect += pass_bytes(ax[k], ay[k], adx[k], ady[k]);
   std::vector<uint8_t> raw;
-  if (!inflate(idat.data() + 2, idat.size() - 2, raw, err)) return false;
+  if (!inflate(idat.data() + 2, idat.size() - 2, raw, err, (size_t)expect)) return false;
+  if (raw.size() < expect) return fail("PNG: image data too short");
   const int bpp = (ch * depth + 7) / 8;  // bytes per complete pixel, for the filters (>= 1)
   im.width = (int)w;
   im.height = (int)h;
@@ -301,8 +325,6 @@ inline bool decode(const std::vector<uint8_t>& d, Image& im, std::string* err) {
   };
   size_t off = 0;
   if (!interlace) return pass(off, 0, 0, 1, 1);
-  static const uint32_t ax[7] = {0, 4, 0, 2, 0, 1, 0}, ay[7] = {0, 0, 4, 0, 2, 0, 1};
-  static const uint32_t adx[7] = {8, 8, 4, 4, 2, 2, 1}, ady[7] = {8, 8, 8, 4, 4, 2, 2};
   for (int k = 0; k < 7; k++)
     if (!pass(off, ax[k], ay[k], adx[k], ady[k])) return false;
   return true;

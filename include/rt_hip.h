@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 7
+#define RT_ABI_VERSION 8
 
 typedef enum rt_status {
   RT_OK = 0,
@@ -226,6 +226,9 @@ typedef struct rt_counters {
   double aux_ms;  /* rt_multi_stats: device time of the gather + unpack; otherwise 0 */
   uint64_t grid_lanes; /* lanes of the last persistent-kernel launch: the resident grid the occupancy
                           query gave that kernel on this device */
+  uint64_t passes;        /* (ABI 8) chunk passes the renders took: a call whose item partial sums exceed
+                             the budget (2 GiB, RT_PARTIAL_BUDGET) renders its chunks in several launches */
+  uint64_t partial_bytes; /* (ABI 8) the partial-sum buffer of the last render call, bytes */
 } rt_counters;
 
 /* What rt_scene_check / rt_scene_upload compiled a descriptor into. */

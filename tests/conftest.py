@@ -15,11 +15,13 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: CPU test taking more than a few seconds")
     # The multi-process GPU test (test_gpu_multiprocess.py) starts its ranks from a forkserver, which
     # must exist before this process touches the GPU: its children are forked from a process that
-    # never initialised HIP, and nothing is exec'ed from one that did.
-    expr = config.getoption("markexpr", default="") or ""
-    if "gpu" in expr and "not gpu" not in expr:
-        import multiprocessing.forkserver
-        multiprocessing.forkserver.ensure_running()
+    # never initialised HIP, and nothing is exec'ed from one that did. Started for every run (it is
+    # cheap), whatever the -m expression: a plain `pytest tests` initialises HIP in earlier GPU tests,
+    # and a forkserver started lazily after that would be a fork+exec from a GPU-initialised process.
+    # The test skips unless RT_FORKSERVER_EARLY is set.
+    import multiprocessing.forkserver
+    multiprocessing.forkserver.ensure_running()
+    os.environ["RT_FORKSERVER_EARLY"] = "1"
 
 
 @pytest.fixture(scope="session")

@@ -28,7 +28,7 @@ def test_every_declared_symbol_is_exported():
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(abi.SIGNATURES), set(names) ^ set(abi.SIGNATURES)
-    assert lib.rt_abi_version() == abi.ABI_VERSION == 7
+    assert lib.rt_abi_version() == abi.ABI_VERSION == 8
 
 
 def test_struct_layout_matches_c(tmp_path):

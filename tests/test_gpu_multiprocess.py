@@ -24,7 +24,11 @@ def _free_port():
 @pytest.mark.parametrize("scene,width,spp,depth", [("cornell_box", 800, 32, 50), ("rtow", 240, 16, 50)],
                          ids=["c2_geometry", "rtow"])
 def test_two_processes_gather_the_one_process_frame(scene, width, spp, depth):
+    import os
+
     import mp_gpu_worker
+    if os.environ.get("RT_FORKSERVER_EARLY") != "1":  # never let multiprocessing start the server after HIP is initialised
+        pytest.skip("the forkserver was not started by conftest.pytest_configure")
     mctx = mp.get_context("forkserver")
     q = mctx.Queue()
     port = _free_port()

@@ -66,3 +66,35 @@ def test_corrupt_files_are_refused(dump, tmp_path):
     p = tmp_path / "bad.hdr"
     p.write_bytes(hdr)
     assert dump(str(p))[:2] == (0, 0)
+
+
+def _png(w, h, ctype, depth, idat):
+    import struct
+    import zlib
+
+    def chunk(tag, data):
+        return struct.pack(">I", len(data)) + tag + data + struct.pack(">I", zlib.crc32(tag + data) & 0xFFFFFFFF)
+    ihdr = struct.pack(">IIBBBBB", w, h, depth, ctype, 0, 0, 0)
+    return b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", ihdr) + chunk(b"IDAT", idat) + chunk(b"IEND", b"")
+
+
+def test_oversized_headers_are_refused_before_allocating(dump, tmp_path):
+    # A header whose dimensions ask for far more than the data holds is refused without allocating its
+    # output (stb_image.h:5124-5129 for PNG, stbi__mad4sizes_valid for HDR); a crafted 2^24 x 2^24 header
+    # with a tiny IDAT used to throw std::bad_alloc out of image::load.
+    import zlib
+    tiny = zlib.compress(b"\0" * 64)
+    cases = {"huge.png": _png(1 << 24, 1 << 24, 2, 8, tiny),
+             "wide.png": _png(1 << 24, 64, 6, 8, tiny),                 # 2^30 / w / 4 < h
+             "short.png": _png(4000, 4000, 2, 8, tiny),                 # allowed size, data far too short
+             "huge.hdr": b"#?RADIANCE\nFORMAT=32-bit_rle_rgbe\n\n-Y 16777216 +X 16777216\n" + b"\x01\x01\x01\x80" * 4}
+    for name, data in cases.items():
+        p = tmp_path / name
+        p.write_bytes(data)
+        w, h, tex = dump(str(p))
+        assert (w, h) == (0, 0) and tex == b"", name
+    # a small valid image still decodes through the capped inflate (the filtered size exactly)
+    ok = tmp_path / "ok.png"
+    ok.write_bytes(_png(3, 2, 2, 8, zlib.compress(b"\0" + bytes(range(9)) + b"\0" + bytes(range(9, 18)))))
+    w, h, tex = dump(str(ok))
+    assert (w, h) == (3, 2) and len(tex) == 18
