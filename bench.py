@@ -49,6 +49,9 @@ VALU_PMC_CLASSES = {  # SQ_INSTS_VALU_* class counters -> the static-mix class t
     "f32_trans": ("SQ_INSTS_VALU_TRANS_F32",),
     "cvt": ("SQ_INSTS_VALU_CVT",),
     "int64": ("SQ_INSTS_VALU_INT64",),
+    # 32-bit integer instructions (round 5: counted, so that under half of the instructions -- moves, selects,
+    # compares, fp32 and the fp64 opcodes no counter singles out -- are priced by the static mix)
+    "int32_other": ("SQ_INSTS_VALU_INT32",),
 }
 
 
@@ -122,7 +125,8 @@ def issue_cycles(counters, mix):
                                                                            "f64_trans": "v_rcp_f64",
                                                                            "f32_trans": "v_rcp_f32",
                                                                            "cvt": "v_cvt_f32_f64",
-                                                                           "int64": "v_lshl_add_u64"}[cl])))
+                                                                           "int64": "v_lshl_add_u64",
+                                                                           "int32_other": "v_add_u32"}[cl])))
             counted += n
     rest_items = [(op, n) for cl, items in by_class.items() if cl not in parts for op, n in items]
     parts["rest"] = (max(0.0, counters["SQ_INSTS_VALU"] - counted), mean_cost(rest_items, 2.0))
@@ -332,9 +336,19 @@ def roofline(key, st, segs, my_samples, elapsed, kern, fp64):
         cycles, parts = issue_cycles(c, mix)
     ach = cycles / avg_s / 1e9
     gui = d.get("grbm_gui_active_per_launch")
+    tr = d.get("trace_avg_ns")
     roof.update({"unit": "G SIMD-cycles/s", "peak": CYCLE_PEAK_G, "achieved": round(ach, 2),
                  "frac": round(ach / CYCLE_PEAK_G, 4), "valu_cycles_per_launch": cycles,
-                 # the same cycles against the clock the GPU actually ran during the profiled launches
+                 # the same cycles over the profiled run's kernel-trace duration (profiles/*_kernel_stats.csv):
+                 # what the committed profile alone gives; frac = frac_profiled * trace_avg / live launch time
+                 "frac_profiled": round(cycles / (tr * 1e-9) / 1e9 / CYCLE_PEAK_G, 4) if tr else None,
+                 "trace_avg_us": round(tr / 1e3, 2) if tr else None,
+                 "profiled_clock_ghz": d.get("profiled_clock_ghz"),
+                 # the live launch at the profiled run's clock: the two runs' clocks differ from box to box
+                 "live_clock_ghz_equiv": (round(d["profiled_clock_ghz"] * tr * 1e-9 / avg_s, 3)
+                                          if tr and d.get("profiled_clock_ghz") else None),
+                 # the same cycles against the cycles the GPU was active during the profiled launches
+                 # (GRBM_GUI_ACTIVE / 8 XCDs): independent of the clock
                  "frac_at_measured_clock": round(cycles / (SIMDS * gui / 8), 4) if gui else None,
                  "cycles_by_class": ({k: {"instr": round(n), "cycles_per_instr": round(cc, 3)} for k, (n, cc) in
                                       parts.items()} if parts else None),
@@ -425,18 +439,41 @@ def main():
     shard = FrameSharding(W, H, world, rank, dev)
     counts = shard.counts
 
+    copy_stream = torch.cuda.Stream(dev)
+
     def run(precision, steps, warmup, timing):
-        """warmup + `steps` timed frames; returns (elapsed s (max over ranks), stats, rank 0's framebuffer)."""
+        """warmup + `steps` timed frames; returns (elapsed s (max over ranks), stats, rank 0's host framebuffer
+        of the last frame)."""
         tdtype = torch.float64 if precision == abi.RT_PREC_F64 else torch.float32
         out, fb = shard.buffers(tdtype)
         params = ctx.params(spp, depth, args.seed, precision, samples_per_item=args.chunk, pool_slots=args.pool,
                             segments_per_launch=args.segments_per_launch,
                             traversal=abi.RT_TRAV_ORDERED if args.traversal == "ordered" else abi.RT_TRAV_AUTO)
+        # SURVEY §8(d): a step ends with the complete linear framebuffer in rank 0's host memory. Two device
+        # framebuffers and two pinned host buffers: frame i's D2H runs on a copy stream while frame i + 1
+        # renders, so only the last frame's copy is exposed; a buffer's next scatter waits for its last copy.
+        fbs = [fb, torch.zeros_like(fb)] if rank == 0 else [None, None]
+        hosts = [torch.empty(fb.shape, dtype=tdtype, pin_memory=True) for _ in range(2)] if rank == 0 else None
+        copied = [None, None]
+        nstep = [0]
 
         def step():
+            k = nstep[0] % 2
+            nstep[0] += 1
+            cur = torch.cuda.current_stream(dev)
+            if copied[k] is not None:
+                cur.wait_event(copied[k])
             # render this rank's tiles on torch's current stream (the default = the HIP null stream); the
             # RCCL gather and rank 0's scatter are queued behind it on the same stream
-            shard.frame(ctx, cam, params, out, fb)
+            shard.frame(ctx, cam, params, out, fbs[k])
+            if rank == 0:
+                ready = torch.cuda.Event()
+                ready.record(cur)
+                copy_stream.wait_event(ready)
+                with torch.cuda.stream(copy_stream):
+                    hosts[k].copy_(fbs[k], non_blocking=True)
+                    copied[k] = torch.cuda.Event()
+                    copied[k].record(copy_stream)
 
         for _ in range(warmup):
             step()
@@ -448,7 +485,7 @@ def main():
         t0 = time.perf_counter()
         for _ in range(steps):
             step()  # stream-ordered: the host enqueues the next frame while the GPU renders this one
-        torch.cuda.synchronize(dev)
+        torch.cuda.synchronize(dev)  # every stream of the device: the last frame's D2H included
         if world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t0
@@ -458,7 +495,7 @@ def main():
             t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
-        return elapsed, st, fb
+        return elapsed, st, (hosts[(nstep[0] - 1) % 2] if rank == 0 else None)
 
     elapsed, st, fb = run(prec, args.steps, args.warmup, args.kernel_timing == "on")
     segs, step_ms, iters = st.segments, st.step_ms, st.iterations
@@ -532,7 +569,11 @@ def main():
                        "image": [W, H], "spp": spp, "max_depth": depth, "tiles": "16x16 round-robin over ranks",
                        "parallelism": f"tiles{world}", "segments_per_sample": round(seg_per_sample, 4),
                        "segments_total": segs_total / args.steps, "kernel_timing": args.kernel_timing,
-                       "rounds_per_frame": iters // max(1, args.steps), "grid_lanes": st.grid_lanes},
+                       "rounds_per_frame": iters // max(1, args.steps), "grid_lanes": st.grid_lanes,
+                       "timed_region": "barrier + sync .. sync + barrier around the steps; a step ends with the "
+                                       "whole linear framebuffer in rank 0's pinned host memory (its D2H on a "
+                                       "copy stream, overlapped with the next frame's render; the last one "
+                                       "inside the region); parity reads that host copy"},
             "roofline": roof,
             "cpu_baseline": cpu,
             "parity": parity,

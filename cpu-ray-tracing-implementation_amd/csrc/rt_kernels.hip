@@ -570,9 +570,15 @@ __global__ __launch_bounds__(kBlock) void k_init(Params<R> p) {
 // ray time is not read here. A LEAN path has no radiance register: emission goes straight into the
 // item's running sum (the same terms, added one by one instead of per sample: a rounding-level
 // regrouping of the pixel's sum).
-template <class R, bool CAMX, bool FLAT = false, bool MOVING = true, class PS>
+// MLDS: `mats` is the kernel's LDS copy of the materials (FlatTrav tables), read with ds_read (a generic
+// pointer that may be LDS or global compiled to flat loads, which wait on both counters).
+// LL ("lambertian + light", round 5): the scene's materials are lambertian and diffuse_light with solid
+// textures (the background's too), and the light an axis-aligned quad (the Cornell configs; host-checked,
+// launch_step): the material is one LDS record lm[mat] = (colour, is_light), and the texture, metal,
+// dielectric, gloss, isotropic and no-light code is compiled out.
+template <class R, bool CAMX, bool FLAT = false, bool MOVING = true, bool MLDS = false, bool LL = false, class PS>
 __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, uint32_t nm = 0,
-                      const Material<R>* mats = nullptr) {
+                      const Material<R>* mats = nullptr, const R4<R>* lm = nullptr) {
   const DevScene<R>& sc = p.sc;
   V<R> add = mkv(R(0), R(0), R(0));
   bool has_add = false, done = false;
@@ -711,25 +717,36 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
            (double)d.z, (double)t, (double)pw.x, (double)pw.y, (double)pw.z, (double)n.x, (double)n.y, (double)n.z,
            (int)front, sc.mats[mat].kind, ty, idx);
 #endif
-    const Material<R>& m = (mats ? mats : sc.mats)[mat];
-    if (m.kind == M_DIFFUSE_LIGHT) {  // material.h:211-215; no scatter
+    using LMat = const __attribute__((address_space(3))) Material<R>;
+    using LRec = const __attribute__((address_space(3))) R4<R>;
+    const Material<R>& m = MLDS ? *(const Material<R>*)((LMat*)mats + mat) : sc.mats[mat];
+    V<R> col{};
+    bool is_light;
+    if constexpr (LL) {
+      LRec* mc = (LRec*)lm + mat;
+      col = mkv(mc->x, mc->y, mc->z);
+      is_light = mc->w != R(0);
+    } else {
+      is_light = m.kind == M_DIFFUSE_LIGHT;
+    }
+    if (is_light) {  // material.h:211-215; no scatter
       if (front) {
-        add = s.thr * tex_sample<R, CAMX>(sc, m.tx, pw, hu, hv);
+        add = s.thr * (LL ? col : tex_sample<R, CAMX>(sc, m.tx, pw, hu, hv));
         has_add = true;
       }
       done = true;
     } else {
-      V<R> att = tex_sample<R, CAMX>(sc, m.tx, pw, hu, hv);
+      V<R> att = LL ? col : tex_sample<R, CAMX>(sc, m.tx, pw, hu, hv);
       const uint32_t bounce = (uint32_t)s.bounce;
       uint32_t js = 0;
       auto U = [&]() { return to_unit<R>(draw_u32(s.ks, dim_scatter(bounce, js++))); };
-      if (m.kind == M_METAL) {  // material.h:85-92
+      if (!LL && m.kind == M_METAL) {  // material.h:85-92
         V<R> dir = unit(reflect(d, n));
         R u1 = U();
         R u2 = U();
         new_d = dir + m.fuzz * unit(on_sphere(u1, u2));
         s.thr = s.thr * att;
-      } else if (m.kind == M_DIELECTRIC) {  // material.h:113-131
+      } else if (!LL && m.kind == M_DIELECTRIC) {  // material.h:113-131
         R ri = front ? fdiv(R(1), m.refr) : m.refr;
         V<R> ud = unit(d);
         R cos_t = fmin(dot(-ud, n), R(1));
@@ -742,7 +759,7 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
         else
           new_d = refract(ud, n, ri);
         s.thr = s.thr * att;
-      } else if (m.kind == M_GLOSS && to_unit<R>(draw_u32(s.ks, dim_scatter(bounce, js))) <= m.spec) {
+      } else if (!LL && m.kind == M_GLOSS && to_unit<R>(draw_u32(s.ks, dim_scatter(bounce, js))) <= m.spec) {
         // gloss, specular branch (material.h:158-167): kDetermined, attenuation 1,
         // direction unit(lerp(smoothness, cosine-hemisphere sample about n, reflect(d_in, n)))
         js++;
@@ -753,8 +770,8 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
         const R tt = m.smooth;
         new_d = unit((R(1) - tt) * diffuse + tt * reflect(d, n));
       } else {  // lambertian (material.h:62-72) / isotropic (material.h:193-200) / gloss diffuse: kRandom
-        if (m.kind == M_GLOSS) js++;  // the specular-choice draw above (material.h:161)
-        const bool iso = m.kind == M_ISOTROPIC;
+        if (!LL && m.kind == M_GLOSS) js++;  // the specular-choice draw above (material.h:161)
+        const bool iso = !LL && m.kind == M_ISOTROPIC;
         const R iso_pdf = R(1) / (R(4) * Num<R>::pi());
         Onb<R> b;
         if (!FLAT && !iso) b = make_onb(n);
@@ -786,7 +803,7 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
         // 73.0). Not for a moving sphere: p_scattered takes the cosine against its non-unit normal,
         // the pdf against the unit one, and the ratio |n| is the reference's (quirk kept)
         bool own_pdf = false;
-        if (ld_here(&Lt->kind) == L_NONE) {
+        if (!LL && ld_here(&Lt->kind) == L_NONE) {
           R u1 = U();
           R u2 = U();
           dir = iso ? unit(on_sphere(u1, u2)) : cos_dir(u1, u2);
@@ -903,17 +920,24 @@ struct LinearTrav {
 #ifndef RT_FLAT_LDS  // flat program (persistent kernels): records and materials copied into LDS
 #define RT_FLAT_LDS 1
 #endif
+#ifndef RT_FLAT_WAVES_F64_LL  // the same for the lambertian + light kernel
+#define RT_FLAT_WAVES_F64_LL 6  // C2 fp64: 5 waves 28.90 ms/frame, 6: 28.08 (r05c; the general kernel at 5: 31.28)
+#endif
+#ifndef RT_FLAT_LL  // flat program: a kernel for lambertian + light scenes (shade LL)
+#define RT_FLAT_LL 1
+#endif
 #ifndef RT_FLAT_NORAD  // flat program: emission added straight into the item's running sum (Path NORAD)
 #define RT_FLAT_NORAD 1
 #endif
 #ifndef RT_FLAT_WAVES_F64  // fp64 flat program: waves per SIMD the register budget is cut for (1: none)
 #define RT_FLAT_WAVES_F64 5
 #endif
-template <class R, bool TLDS = false>
+template <class R, bool TLDS = false, bool LL = false>
 struct FlatTrav {
   static constexpr bool kTablesLds = TLDS;  // persistent kernel: Tables in LDS (fill, run_lds)
+  static constexpr bool kLL = LL;           // lambertian + light scene (shade LL; the lm table)
   static constexpr int kStack = 0;
-  static constexpr int kWaves = sizeof(R) == 4 ? RT_FLAT_WAVES : RT_FLAT_WAVES_F64;
+  static constexpr int kWaves = sizeof(R) == 4 ? RT_FLAT_WAVES : (LL ? RT_FLAT_WAVES_F64_LL : RT_FLAT_WAVES_F64);
   static constexpr int kLdsNodes = 0;
   static constexpr bool kFlat = true;
   static constexpr bool kWide = false;
@@ -928,11 +952,14 @@ struct FlatTrav {
   }
   // the scene's small tables copied into LDS (persistent kernel, RT_FLAT_LDS): the hit's record and
   // material are then LDS reads instead of dependent global loads
-  static constexpr uint32_t kLdsQuads = 64, kLdsBoxes = 16, kLdsMats = 32;
+  // (the LL kernel's tables are smaller, so a 256-lane block's LDS -- tables plus the fp64 cold path state,
+  // ~27 KB with the general sizes -- leaves room for 6 blocks per CU)
+  static constexpr uint32_t kLdsQuads = LL ? 16 : 64, kLdsBoxes = LL ? 8 : 16, kLdsMats = LL ? 16 : 32;
   struct Tables {
     FlatQuadT<R> q[kLdsQuads];
     FlatBoxT<R> b[kLdsBoxes];
-    Material<R> m[kLdsMats];
+    Material<R> m[LL ? 1 : kLdsMats];
+    R4<R> lm[LL ? kLdsMats : 1];  // LL: (solid colour, 1 for diffuse_light)
   };
   __host__ __device__ __forceinline__ static bool tables_fit(const DevScene<R>& sc) {
     return sc.n_flatq[0] + sc.n_flatq[1] + sc.n_flatq[2] <= kLdsQuads && sc.n_flatb <= kLdsBoxes &&
@@ -942,7 +969,14 @@ struct FlatTrav {
     const uint32_t nq = sc.n_flatq[0] + sc.n_flatq[1] + sc.n_flatq[2];
     for (uint32_t j = threadIdx.x; j < nq; j += kBlock) tb.q[j] = sc.flatq[j];
     for (uint32_t j = threadIdx.x; j < sc.n_flatb; j += kBlock) tb.b[j] = sc.flatb[j];
-    for (uint32_t j = threadIdx.x; j < sc.n_mats; j += kBlock) tb.m[j] = sc.mats[j];
+    for (uint32_t j = threadIdx.x; j < sc.n_mats; j += kBlock) {
+      if constexpr (LL) {
+        const Material<R>& m = sc.mats[j];
+        tb.lm[j] = R4<R>{m.tx.c0[0], m.tx.c0[1], m.tx.c0[2], m.kind == M_DIFFUSE_LIGHT ? R(1) : R(0)};
+      } else {
+        tb.m[j] = sc.mats[j];
+      }
+    }
   }
   template <class PS>
   __device__ __forceinline__ static void run_lds(const DevScene<R>& sc, const Tables& tb, const PS& s, R& t,
@@ -1259,7 +1293,7 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
           atomicOr(q.fault, 1u);
           break;
         }
-        if (!shade<R, CAMX, true>(q, s, t, e, inst, nm, flat_tb->m)) break;
+        if (!shade<R, CAMX, true, true, true, Trav::kLL>(q, s, t, e, inst, nm, flat_tb->m, flat_tb->lm)) break;
       }
     } else {
 #if RT_PARAM_RELOAD
@@ -1796,15 +1830,26 @@ constexpr bool family_built(KernelFamily f) {
   return RT_DEV_ONLY == 0 || (RT_DEV_ONLY == 1 && f == KF_FLAT) || (RT_DEV_ONLY == 2 && f == KF_WIDE) ||
          (RT_DEV_ONLY == 3 && f == KF_LIN_VOL);
 }
+// a lambertian + diffuse_light scene with solid textures (a background too) and an axis-aligned quad light (the
+// Cornell configs): the flat kernel's LL form (shade LL)
+bool lamb_light_scene(const SceneHeader& h) {
+  const uint32_t ok_m = (1u << M_LAMBERTIAN) | (1u << M_DIFFUSE_LIGHT);
+  return (h.mat_kinds & ~ok_m) == 0 && (h.tex_kinds & ~(1u << T_SOLID)) == 0 && h.light_kind == L_QUAD &&
+         h.light_aligned != 0;
+}
 template <class R>
-void launch_step(const Params<R>& p, KernelFamily fam, int stack, uint32_t grid, hipStream_t st) {
+void launch_step(const Params<R>& p, KernelFamily fam, bool ll, int stack, uint32_t grid, hipStream_t st) {
   switch (fam) {
     case KF_FLAT:
       if constexpr (family_built(KF_FLAT)) {
-        if (RT_FLAT_LDS && p.persist && FlatTrav<R, true>::tables_fit(p.sc))
-          launch_k<R, FlatTrav<R, true>>(p, grid, st);
-        else
+        if (RT_FLAT_LDS && p.persist && FlatTrav<R, true>::tables_fit(p.sc)) {
+          if (RT_FLAT_LL && ll && FlatTrav<R, true, true>::tables_fit(p.sc))
+            launch_k<R, FlatTrav<R, true, true>>(p, grid, st);
+          else
+            launch_k<R, FlatTrav<R, true>>(p, grid, st);
+        } else {
           launch_k<R, FlatTrav<R>>(p, grid, st);
+        }
       }
       return;
     case KF_LIN_QUAD:
@@ -1936,6 +1981,7 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     const KernelFamily fam = kernel_family(hdr, cam->mode, persist, prm->traversal == RT_TRAV_ORDERED);
     if (!family_built(fam))
       return set_err(c, RT_ERR_UNSUPPORTED, std::string("this build (RT_DEV_ONLY) has no ") + family_name(fam) + " kernels");
+    const bool ll = lamb_light_scene(hdr);
     uint32_t P = prm->pool_slots > 0 ? (uint32_t)prm->pool_slots
                  : persist       ? kAutoPersistLanes
                                  : (f64 ? kAutoPool64 : kAutoPool32);
@@ -2042,11 +2088,11 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
           hipEvent_t e0 = take_event(c, ev0 + ev), e1 = take_event(c, ev0 + ev + 1);
           if (!e0 || !e1) return set_err(c, RT_ERR_HIP, "hipEventCreate failed");
           RT_HIP(c, hipEventRecord(e0, st));
-          launch_step<R>(p, fam, cs.stack_need, grid, st);
+          launch_step<R>(p, fam, ll, cs.stack_need, grid, st);
           RT_HIP(c, hipEventRecord(e1, st));
           ev += 2;
         } else {
-          launch_step<R>(p, fam, cs.stack_need, grid, st);
+          launch_step<R>(p, fam, ll, cs.stack_need, grid, st);
         }
         RT_HIP(c, hipGetLastError());
         c->last.grid_lanes = t_grid_lanes;
@@ -2076,11 +2122,11 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
               hipEvent_t e0 = take_event(c, ev0 + ev), e1 = take_event(c, ev0 + ev + 1);
               if (!e0 || !e1) return set_err(c, RT_ERR_HIP, "hipEventCreate failed");
               RT_HIP(c, hipEventRecord(e0, st));
-              launch_step<R>(p, fam, cs.stack_need, grid, st);
+              launch_step<R>(p, fam, ll, cs.stack_need, grid, st);
               RT_HIP(c, hipEventRecord(e1, st));
               ev += 2;
             } else {
-              launch_step<R>(p, fam, cs.stack_need, grid, st);
+              launch_step<R>(p, fam, ll, cs.stack_need, grid, st);
             }
             launches++;
             iters++;

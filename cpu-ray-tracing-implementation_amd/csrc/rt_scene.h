@@ -309,6 +309,11 @@ struct SceneHeader {
   uint32_t wide_big;     // primitives at the head of the word stream tested before the tree (huge boxes)
   uint32_t has_wnodesh;  // the WNodeH form of the same tree is present (n_wnodes nodes from off_wnodesh)
   uint64_t off_wnodesh;
+  // what shading can meet (round 5: kernels specialised for lambertian + diffuse_light scenes)
+  uint32_t mat_kinds;   // bit M_* of every material kind
+  uint32_t tex_kinds;   // bit T_* of every material's texture kind (the background's too)
+  int32_t light_kind;   // L_* of the importance-sampling light
+  int32_t light_aligned;
 };
 
 }  // namespace rtd

@@ -828,6 +828,13 @@ SceneHeader pack(std::vector<unsigned char>& blob, const std::vector<Q>& q, cons
   h.n_mats = (uint32_t)m.size();
   h.n_texs = (uint32_t)x.size();
   h.num_instances = (int32_t)in.size();
+  for (const auto& mm : m) {
+    h.mat_kinds |= 1u << (mm.kind & 31);
+    h.tex_kinds |= 1u << (mm.tx.kind & 31);
+  }
+  for (const auto& tx : x) h.tex_kinds |= 1u << (tx.kind & 31);  // the background's texture (and the rest)
+  h.light_kind = light.kind;
+  h.light_aligned = light.aligned;
   return h;
 }
 

@@ -80,9 +80,11 @@ def main():
     # the dominant kernel instantiation (longest total time in the kernel trace) and its static VALU opcode
     # mix (scripts/valu_static_mix.py), for bench.py's issue-cycle model
     mix_file = None
+    trace_avg = None
     if stats:
         with open(stats[0]) as fh:
             top = max(csv.DictReader(fh), key=lambda r: float(r["TotalDurationNs"]))
+        trace_avg = float(top["AverageNs"])
         kname = top["Name"][5:] if top["Name"].startswith("void ") else top["Name"]
         kname = kname.split("((anonymous namespace)::Params")[0]
         sys.path.insert(0, os.path.join(REPO, "scripts"))
@@ -99,6 +101,10 @@ def main():
              "valu_per_launch": valu,
              "valu_issue_frac_measured_clock": round(valu * 2 / (1024 * gui / 8), 4) if gui else None,
              "grbm_gui_active_per_launch": gui,
+             # the dominant kernel's average duration in the --kernel-trace pass, and the shader clock the
+             # profiled launches ran at: GPU-active cycles per XCD (GRBM_GUI_ACTIVE / 8) over that duration
+             "trace_avg_ns": trace_avg,
+             "profiled_clock_ghz": round(gui / 8 / trace_avg, 4) if gui and trace_avg else None,
              # active lanes per issued VALU instruction (rocprof's VALUUtilization)
              "valu_lane_util": (round(fam_mean("SQ_THREAD_CYCLES_VALU")[0] / (64 * fam_mean("SQ_ACTIVE_INST_VALU")[0]), 4)
                                 if fam_mean("SQ_THREAD_CYCLES_VALU")[0] and fam_mean("SQ_ACTIVE_INST_VALU")[0] else None),
