@@ -143,6 +143,10 @@ CONFIGS = {
     "c3": ("rtow", 1200, 1.5, 512, 50),
     "c4": ("sponza", 1920, 16.0 / 9.0, 256, 5),
     "c5": ("cornell_box_with_volume", 3840, 16.0 / 9.0, 4096, 5),
+    # SURVEY §8(f) rows (not BASELINE configs): main.cc's own sizes and spp, on the CAMX kernels
+    "f1": ("skybox_and_fisheye", 600, 1.0, 500, 5),       # main.cc:174-183: fisheye camera, picture skybox
+    "f2": ("skybox_and_motion_blur", 600, 1.0, 500, 5),   # main.cc:185-196: earthmap texture, moving sphere
+    "f3": ("perlin_texture_ball", 600, 1.0, 500, 5),      # main.cc:402-437: perlin textures over 400 boxes
 }
 
 
@@ -427,6 +431,9 @@ def main():
 
     scene_name, width, aspect, spp, depth = CONFIGS[args.config]
     asset = sponza_asset()[1] if scene_name == "sponza" else None
+    if scene_name.startswith("skybox"):  # the reference's earthmap.jpg (its bathroom.exr: no EXR decoder, magenta)
+        os.environ.setdefault("RT_ASSETS", os.path.join(REPO, "tests", "golden", "assets"))
+        asset = "the reference's assets/earthmap.jpg; bathroom.exr is not decodable (tinyexr absent): magenta skybox"
     # the scene exactly as the drop-in camera::render flattens it (C++ plugin surface, main.cc:198-225)
     cs = plugin.ConfigScene(scene_name, width, aspect)
     cam = cs.cam

@@ -39,6 +39,21 @@ namespace rtd {
 #ifndef RT_WIDE_PREFETCH  // a triangle's words loaded with the record's first word (C4 358.9 -> 357.2 ms)
 #define RT_WIDE_PREFETCH 1
 #endif
+// The extended (CAMX) kernels' heavy, rarely taken code -- fp64 OCML trigonometry (sphere_uv, the fisheye
+// camera), the noise textures -- as real calls (round 5): inlined, their temporaries sized the whole kernel
+// (~290 registers, 1 wave per SIMD); called, the loop keeps its own budget and the live state is saved
+// around the call only when it is taken.
+#ifndef RT_EXT_NOINLINE
+#define RT_EXT_NOINLINE 1
+#endif
+#if RT_EXT_NOINLINE
+#define RT_EXT_FN __device__ __attribute__((noinline))
+#else
+#define RT_EXT_FN __device__ __forceinline__
+#endif
+#ifndef RT_MIX_SELECT  // the light / material halves of the mixture pdf (pdf.h:52-56) as one select path: 1 in
+#define RT_MIX_SELECT 1  // the flat program (C2 fp64 28.33 -> 28.15 ms/frame, fp32 18.83 -> 18.49, r05e), 2 in every kernel
+#endif
 #ifndef RT_LIGHT_PDF_F64  // fp64 axis-aligned light pdf by one reciprocal (light_pdf_aligned, round 4)
 #define RT_LIGHT_PDF_F64 1
 #endif
@@ -1069,15 +1084,26 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
   const R tmin = R(0.001);
   const float tmin_box = F64 ? 0.00099f : 0.001f;
   const V<float> o = mkv((float)ro.x, (float)ro.y, (float)ro.z);
-  const V<float> inv = box_inv(mkv((float)rd.x, (float)rd.y, (float)rd.z));
+  V<float> inv = box_inv(mkv((float)rd.x, (float)rd.y, (float)rd.z));
   [[maybe_unused]] float wx = 0.f, wy = 0.f, wz = 0.f;  // fp64: the slab widening per axis
   if constexpr (F64) {
-    auto widen = [](double dlt, float iv) {
+    // A direction component that is 0 in float (an exactly axis-parallel ray: a cosine sample with r2 = 0,
+    // random_cosine_direction's (0, 1, 0), about 10 times per C4 frame) gives inv = inf, and an infinite
+    // widening made that axis cull nothing: the ray visited most of the tree (C4 fp64: single items of
+    // 260-400 ms, the frame's tail, r05n/r05o). Such an axis takes inv = +-2^100 instead, and the widening
+    // covers the origin's rounding plus an ulp of it (a plane exactly through the float origin):
+    // (|delta| + |o| 2^-22 + 2^-126) 2^100. Any box the exact test accepts still passes.
+    auto widen = [](double dlt, float oa, float& iv) {
+      if (!(fabsf(iv) < 1.2676506002282294e30f)) {  // 2^100 (inf, or a float direction that underflowed)
+        iv = __builtin_copysignf(1.2676506002282294e30f, iv);
+        return ((float)fabs(dlt) + fabsf(oa) * 2.384185791015625e-07f + 1.1754943508222875e-38f) *
+               1.2676506002282294e30f * (1.0f + 9.5367431640625e-07f);
+      }
       return dlt == 0.0 ? 0.f : fabsf((float)dlt * iv) * (1.0f + 9.5367431640625e-07f);
     };
-    wx = widen(ro.x - (double)o.x, inv.x);
-    wy = widen(ro.y - (double)o.y, inv.y);
-    wz = widen(ro.z - (double)o.z, inv.z);
+    wx = widen(ro.x - (double)o.x, o.x, inv.x);
+    wy = widen(ro.y - (double)o.y, o.y, inv.y);
+    wz = widen(ro.z - (double)o.z, o.z, inv.z);
   }
   const WW* prims = LDSN ? lds_prims : sc.wprims;
   uint32_t keep_going = 0;  // pause at or below this many traversing lanes
@@ -1331,6 +1357,9 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
     ry.fresh = 0;
   }
   bool done = false;
+#ifdef RT_WIDE_DEBUG_LONG
+  uint32_t dbg_visits = 0;
+#endif
   // Speculative while-while (Aila & Laine 2009), for trees in HBM: a lane that reaches a leaf
   // postpones it and keeps traversing until every traversing lane of the wave holds one, so the
   // leaf tests run with the wave's lanes together instead of a few at a time, and node fetches
@@ -1343,6 +1372,12 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
     uint32_t leaf = 0u;  // the postponed leaf (a leaf code is never 0)
     while (have) {
       RT_WIDE_STAT(0);
+#ifdef RT_WIDE_DEBUG_LONG  // development: a traversal far longer than the tree warrants
+      if (++dbg_visits == 20000u)
+        printf("[long] o=(%.17g %.17g %.17g) d=(%.17g %.17g %.17g) inv=(%g %g %g) w=(%g %g %g) tmax=%g sp=%d cur=%u\n",
+               (double)ro.x, (double)ro.y, (double)ro.z, (double)rd.x, (double)rd.y, (double)rd.z, inv.x, inv.y, inv.z,
+               wx, wy, wz, (double)tmax, sp, cur);
+#endif
       if (cur & kLeafBit) {
         if (leaf) break;  // a second leaf: test the first, come back with this one
         leaf = cur;
@@ -1725,7 +1760,7 @@ __device__ __forceinline__ double perlin_noise(const double* tb, double px, doub
   return accum;
 }
 // perlin_texture::sample (texture.h:84-88) with turb(7, p / scale) (noise.h:44-54)
-__device__ __forceinline__ double perlin_texture(const double* tb, double scale, double px, double py, double pz) {
+RT_EXT_FN double perlin_texture(const double* tb, double scale, double px, double py, double pz) {
 #pragma clang fp contract(off)  // the reference's rounding: the sin hash amplifies any FMA
   double qx = px / scale, qy = py / scale, qz = pz / scale;
   double accum = 0, weight = 1.0;
@@ -1740,7 +1775,7 @@ __device__ __forceinline__ double perlin_texture(const double* tb, double scale,
 }
 // value_noise::noise (noise.h:109-131): trilinear over a float table indexed without wrapping;
 // an index outside the table (undefined behaviour in the reference) reads 0
-__device__ __forceinline__ double value_noise(const double* tb, uint32_t n, double px, double py, double pz) {
+RT_EXT_FN double value_noise(const double* tb, uint32_t n, double px, double py, double pz) {
 #pragma clang fp contract(off)  // the reference's rounding: the sin hash amplifies any FMA
   const double fx = floor(px), fy = floor(py), fz = floor(pz);
   const double nn = (double)n, n3 = nn * nn * nn;
@@ -1771,7 +1806,7 @@ __device__ __forceinline__ void cell_hash(double ux, double uy, double uz, doubl
 }
 // noise.h:147-167 (worley: squared distance to the nearest feature point) and 178-200 (voronoi:
 // a hash of the nearest feature point), float distances as in the reference
-__device__ __forceinline__ double cell_noise(bool voronoi, double px, double py, double pz) {
+RT_EXT_FN double cell_noise(bool voronoi, double px, double py, double pz) {
 #pragma clang fp contract(off)  // the reference's rounding: the sin hash amplifies any FMA
   const double fx = floor(px), fy = floor(py), fz = floor(pz);
   float min_dist = 3.40282347e+38f, color = 0.0f;
@@ -1800,7 +1835,7 @@ __device__ __forceinline__ double cell_noise(bool voronoi, double px, double py,
 // cameras); the base kernels only contain the solid and checker textures.
 // sphere::get_sphere_uv (sphere.h:90-95) of a unit vector
 template <class R>
-__device__ __forceinline__ void sphere_uv(V<R> n, double& u, double& v) {
+RT_EXT_FN void sphere_uv(V<R> n, double& u, double& v) {
   const double theta = acos(-(double)n.y);
   const double phi = atan2(-(double)n.z, (double)n.x) + 3.1415926535897932385;
   u = phi / (2 * 3.1415926535897932385);
@@ -1934,7 +1969,8 @@ __device__ __forceinline__ double light_pdf_aligned(const double* f, V<double> o
   const double dd = d.x * d.x + d.y * d.y + d.z * d.z;
   return ((th * th) * dd) * (dd * frsq_nz(dd)) * fabs(rA) * f[7];
 }
-template <class R>
+// SEL: the fp32 sampled directions (dir from light_random) by select, not a branch (RT_MIX_SELECT)
+template <class R, bool SEL = false>
 __device__ __forceinline__ R light_pdf(const Light<R>* Lp, V<R> o, V<R> dir, bool sampled = false) {
   const int32_t kind = ld_here(&Lp->kind);
   if (kind == L_QUAD) {
@@ -1954,7 +1990,7 @@ __device__ __forceinline__ R light_pdf(const Light<R>* Lp, V<R> o, V<R> dir, boo
         }
       }
     }
-    if (sizeof(R) == 4 && sampled) {
+    if (sizeof(R) == 4 && sampled && !(SEL && aligned)) {
       t = R(1);
       hit = true;
     } else if (aligned) {  // uniform branch
@@ -1967,6 +2003,13 @@ __device__ __forceinline__ R light_pdf(const Light<R>* Lp, V<R> o, V<R> dir, boo
         case 4: hit = aquad_t<0, 1, 2>(af.f, o, dir, inv, R(0.001), Num<R>::inf(), t); break;
         case 5: hit = aquad_t<1, 2, 0>(af.f, o, dir, inv, R(0.001), Num<R>::inf(), t); break;
         default: hit = aquad_t<0, 2, 1>(af.f, o, dir, inv, R(0.001), Num<R>::inf(), t); break;
+      }
+      if constexpr (sizeof(R) == 4 && SEL) {  // the sampled directions by select, not a branch
+        t = sampled ? R(1) : t;
+        hit = hit | sampled;
+        const Quad<R> q = ld_here(&Lp->quad);
+        const R pdf = fdiv(t * t * dot(dir, dir), fabs(dot(unit(dir), ld3(q.n))) * q.area);
+        return hit ? pdf : R(0);
       }
     } else {
       hit = quad_t(ld_here(&Lp->quad), o, dir, R(0.001), Num<R>::inf(), t);

@@ -252,6 +252,9 @@ struct Path {
 #if RT_CAM_BASE
   V<double> cb_;  // (dir00 + x du) + y dv of the item's pixel (pixel_base)
 #endif
+#ifdef RT_ITEM_CLOCKS
+  uint64_t t0_;  // development: wall clock at the item's start
+#endif
   enum { kAcc = 0, kKa = 3, kItem, kSample, kSend, kXy };
   __device__ __forceinline__ static uint32_t& w(int k) { return cold_words()[k * kBlock]; }
   __device__ __forceinline__ V<R> acc() const {
@@ -451,8 +454,15 @@ __device__ __forceinline__ uint32_t send_of(const Params<R>& p, const PS& s) {
 }
 
 // A new work item for the slot: its pixel and that pixel's RNG key.
+#ifdef RT_ITEM_CLOCKS
+// development build (scripts/dev_item_clocks.py): each item's duration in wall-clock ticks (100 MHz), by item
+__device__ uint32_t* g_item_clk;
+#endif
 template <class R, class PS>
 __device__ __forceinline__ void begin_item(const Params<R>& p, PS& s, uint32_t item) {
+#ifdef RT_ITEM_CLOCKS
+  s.t0_ = wall_clock64();
+#endif
   uint32_t lchunk, first, end;
   item_range(p, item, lchunk, first, end);
   const uint32_t xy = p.pixmap[item - lchunk * p.npix];
@@ -469,7 +479,7 @@ __device__ __forceinline__ void begin_item(const Params<R>& p, PS& s, uint32_t i
 // camera::generate_ray for the orthonormal, fisheye and lens models (camera.h:252-290), reading
 // its fields from device memory. Only the CAMX kernel instantiations contain it, so the
 // perspective kernels' registers are not shaped by it.
-__device__ __forceinline__ void camera_ray(const CamDev* cp, uint32_t ks, uint32_t x, uint32_t y, double ox,
+RT_EXT_FN void camera_ray(const CamDev* cp, uint32_t ks, uint32_t x, uint32_t y, double ox,
                                         double oy, V<double>& o, V<double>& d, double& tm) {
   const int32_t mode = ld_uniform(&cp->mode, 0);
   const V<double> du = ld_uniform(&cp->du, 0), dv = ld_uniform(&cp->dv, 0);
@@ -576,10 +586,15 @@ __global__ __launch_bounds__(kBlock) void k_init(Params<R> p) {
 // textures (the background's too), and the light an axis-aligned quad (the Cornell configs; host-checked,
 // launch_step): the material is one LDS record lm[mat] = (colour, is_light), and the texture, metal,
 // dielectric, gloss, isotropic and no-light code is compiled out.
-template <class R, bool CAMX, bool FLAT = false, bool MOVING = true, bool MLDS = false, bool LL = false, class PS>
+// NL ("no light", round 5): the materials are lambertian, metal and dielectric (solid and checker textures)
+// and there is no importance-sampling light (RTOW, C3; host-checked): the emission, gloss, isotropic and
+// light-mixture code is compiled out.
+template <class R, bool CAMX, bool FLAT = false, bool MOVING = true, bool MLDS = false, bool LL = false,
+          bool NL = false, class PS>
 __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, uint32_t nm = 0,
                       const Material<R>* mats = nullptr, const R4<R>* lm = nullptr) {
   const DevScene<R>& sc = p.sc;
+  constexpr bool kMixSel = RT_MIX_SELECT == 2 || (RT_MIX_SELECT == 1 && FLAT);
   V<R> add = mkv(R(0), R(0), R(0));
   bool has_add = false, done = false;
   V<R> new_o = s.o, new_d = s.d;
@@ -727,7 +742,7 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
       col = mkv(mc->x, mc->y, mc->z);
       is_light = mc->w != R(0);
     } else {
-      is_light = m.kind == M_DIFFUSE_LIGHT;
+      is_light = !NL && m.kind == M_DIFFUSE_LIGHT;
     }
     if (is_light) {  // material.h:211-215; no scatter
       if (front) {
@@ -759,7 +774,7 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
         else
           new_d = refract(ud, n, ri);
         s.thr = s.thr * att;
-      } else if (!LL && m.kind == M_GLOSS && to_unit<R>(draw_u32(s.ks, dim_scatter(bounce, js))) <= m.spec) {
+      } else if (!LL && !NL && m.kind == M_GLOSS && to_unit<R>(draw_u32(s.ks, dim_scatter(bounce, js))) <= m.spec) {
         // gloss, specular branch (material.h:158-167): kDetermined, attenuation 1,
         // direction unit(lerp(smoothness, cosine-hemisphere sample about n, reflect(d_in, n)))
         js++;
@@ -770,8 +785,8 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
         const R tt = m.smooth;
         new_d = unit((R(1) - tt) * diffuse + tt * reflect(d, n));
       } else {  // lambertian (material.h:62-72) / isotropic (material.h:193-200) / gloss diffuse: kRandom
-        if (!LL && m.kind == M_GLOSS) js++;  // the specular-choice draw above (material.h:161)
-        const bool iso = !LL && m.kind == M_ISOTROPIC;
+        if (!LL && !NL && m.kind == M_GLOSS) js++;  // the specular-choice draw above (material.h:161)
+        const bool iso = !LL && !NL && m.kind == M_ISOTROPIC;
         const R iso_pdf = R(1) / (R(4) * Num<R>::pi());
         Onb<R> b;
         if (!FLAT && !iso) b = make_onb(n);
@@ -803,7 +818,7 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
         // 73.0). Not for a moving sphere: p_scattered takes the cosine against its non-unit normal,
         // the pdf against the unit one, and the ratio |n| is the reference's (quirk kept)
         bool own_pdf = false;
-        if (!LL && ld_here(&Lt->kind) == L_NONE) {
+        if (NL || (!LL && ld_here(&Lt->kind) == L_NONE)) {
           R u1 = U();
           R u2 = U();
           dir = iso ? unit(on_sphere(u1, u2)) : cos_dir(u1, u2);
@@ -814,12 +829,17 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
           R u1 = U();
           R u2 = U();
           const bool from_light = c < R(0.5);
-          if (from_light)
+          if constexpr (kMixSel) {  // both generators for every lane, one select (no divergent branch)
+            const V<R> dl = light_random(Lt, pw, u1, u2);
+            const V<R> dc = iso ? unit(on_sphere(u1, u2)) : cos_dir(u1, u2);
+            dir = from_light ? dl : dc;
+          } else if (from_light) {
             dir = light_random(Lt, pw, u1, u2);
-          else
+          } else {
             dir = iso ? unit(on_sphere(u1, u2)) : cos_dir(u1, u2);
+          }
           R mp = iso ? iso_pdf : fmax(R(0), div_pi(cos_n(unit(dir))));
-          pv = R(0.5) * light_pdf(Lt, pw, dir, from_light) + R(0.5) * mp;
+          pv = R(0.5) * light_pdf<R, kMixSel>(Lt, pw, dir, from_light) + R(0.5) * mp;
         }
         if (own_pdf) {
           s.thr = s.thr * att;
@@ -867,6 +887,9 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
     s.set_acc(acc);
   } else {
     const uint32_t item = s.item();
+#ifdef RT_ITEM_CLOCKS
+    if (g_item_clk) g_item_clk[item] = (uint32_t)(wall_clock64() - s.t0_);
+#endif
     R* dst = p.partial + 3ull * item;
     dst[0] = acc.x;
     dst[1] = acc.y;
@@ -879,6 +902,9 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
     }
     begin_item(p, s, nx);
   }
+  // (round 5: regenerating the finished lanes of a wave in batches -- a lane waiting idle until 16 or 32 of
+  // its wave's lanes had finished -- was slower, C2 fp64 28.33 -> 28.46 / 29.95 ms/frame, r05e: the lanes a
+  // wait idles in trace and shade cost more than the regeneration's 41 % lane use)
   begin_sample<R, CAMX>(p, s);
   return true;
 }
@@ -1038,15 +1064,32 @@ struct StackTrav {
 #ifndef RT_WIDE_WAVES_GLOBAL_F64  // tree in HBM (C4 fp64: 3 waves 599.8, 4: 555.0, 5: 567.3)
 #define RT_WIDE_WAVES_GLOBAL_F64 4
 #endif
+#ifndef RT_WIDE_WAVES_GLOBAL_F64_LL  // the LL form (116 VGPRs at 4 waves): C4 fp64 at 4 waves 522.4 ms/frame, 5: 490.6
+#define RT_WIDE_WAVES_GLOBAL_F64_LL 5  // (r05g; the general kernel at 4: 526.7)
+#endif
+#ifndef RT_WIDE_WAVES_F64_NL  // the NL form over an LDS tree, fp64 (116 VGPRs at 4 waves)
+#define RT_WIDE_WAVES_F64_NL 4
+#endif
+#ifndef RT_WIDE_NL  // a wide kernel for sphere scenes without a light (shade NL)
+#define RT_WIDE_NL 1
+#endif
+#ifndef RT_WIDE_LL  // a wide kernel for lambertian + light triangle/quad scenes (shade LL)
+#define RT_WIDE_LL 1
+#endif
 #ifndef RT_WIDE_LEAN  // the wide kernels keep the lean path state (Path LEAN)
 #define RT_WIDE_LEAN 1
 #endif
-template <class R, bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN>
+// LL: a lambertian + light scene (shade LL; the material table `Lm` in static LDS)
+template <class R, bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN, bool LL = false, bool NL = false>
 struct WideTrav {
+  static constexpr bool kLL = LL;
+  static constexpr bool kNL = NL;  // no light (shade NL)
+  static constexpr uint32_t kLdsMats = 16;
   static constexpr int kStack = 0;
   static constexpr int kLdsNodes = 0;
   static constexpr int kWaves = sizeof(R) == 4 ? (LDSN ? RT_WIDE_WAVES : RT_WIDE_WAVES_GLOBAL)
-                                               : (LDSN ? RT_WIDE_WAVES_F64 : RT_WIDE_WAVES_GLOBAL_F64);
+                                               : (LDSN ? (NL ? RT_WIDE_WAVES_F64_NL : RT_WIDE_WAVES_F64)
+                                                       : (LL ? RT_WIDE_WAVES_GLOBAL_F64_LL : RT_WIDE_WAVES_GLOBAL_F64));
   static constexpr bool kFlat = false;
   static constexpr bool kWide = true;
   static constexpr bool kColdLds = false;  // its LDS holds the tree and the stacks
@@ -1216,6 +1259,19 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
     __syncthreads();
     flat_tb = &tb;
   }
+  // the wide LL kernels: the materials as (colour, is_light) records in LDS (shade LL)
+  [[maybe_unused]] const R4<R>* wlm = nullptr;
+  if constexpr (Trav::kWide) {
+    if constexpr (Trav::kLL) {
+      __shared__ R4<R> wlm_tab[Trav::kLdsMats];
+      for (uint32_t j = threadIdx.x; j < p.sc.n_mats; j += kBlock) {
+        const Material<R>& m = p.sc.mats[j];
+        wlm_tab[j] = R4<R>{m.tx.c0[0], m.tx.c0[1], m.tx.c0[2], m.kind == M_DIFFUSE_LIGHT ? R(1) : R(0)};
+      }
+      __syncthreads();
+      wlm = wlm_tab;
+    }
+  }
   uint32_t item0 = blockIdx.x * kBlock + threadIdx.x;
   if (p.persist == 2) {
     if ((threadIdx.x & 63) == 0) {
@@ -1267,12 +1323,12 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
 #ifdef RT_SECTION_CLOCKS
         RT_WIDE_STAT(4);
         const uint64_t c1 = clock64();
-        const bool more = shade<R, CAMX, false, Trav::kMoving>(q, s, t, e, -1, 0);
+        const bool more = shade<R, CAMX, false, Trav::kMoving, Trav::kLL, Trav::kLL, Trav::kNL>(q, s, t, e, -1, 0, nullptr, wlm);
         if (__lane_id() == (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1)
           atomicAdd(wide_stats_lds() + 7, (unsigned long long)(clock64() - c1));
         if (!more) break;
 #else
-        if (!shade<R, CAMX, false, Trav::kMoving>(q, s, t, e, -1, 0)) break;
+        if (!shade<R, CAMX, false, Trav::kMoving, Trav::kLL, Trav::kLL, Trav::kNL>(q, s, t, e, -1, 0, nullptr, wlm)) break;
 #endif
       }
     } else if constexpr (Trav::kTablesLds) {
@@ -1355,8 +1411,21 @@ template <class R, class Trav, bool CAMX>
 __global__ __launch_bounds__(kBlock) void k_persist(Params<R> p) {
   persist_body<R, Trav, CAMX>(p);
 }
+// CAMX kernels (non-perspective cameras, picture and procedural textures) take RT_CAMX_WAVES (fp32) and
+// RT_CAMX_WAVES_F64 waves per SIMD. Round 4 left them unbudgeted: ~290 registers, 1 wave per SIMD. With the
+// heavy code as calls (RT_EXT_FN) the §8(f) configs, ms/frame at 1 wave (round 4) / 2 / 3 / 4 waves (r05f,
+// r05g): fisheye f64 14.8 / 11.0 / 13.5 / 16.2, f32 14.2 / 10.7 / 8.6 / 8.8; earth f64 10.5 / 6.6 / 8.9 /
+// 11.1, f32 9.9 / 6.2 / 4.9 / 4.8; perlin f64 148 / 81 / 70 / 79, f32 128 / 69 / 50 / 43. The fp64 linear
+// programs need ~144 registers without any CAMX code, so 4 waves spills there.
+#ifndef RT_CAMX_WAVES
+#define RT_CAMX_WAVES 4
+#endif
+#ifndef RT_CAMX_WAVES_F64
+#define RT_CAMX_WAVES_F64 2
+#endif
+#define RT_CAMX_W(R) (sizeof(R) == 8 ? RT_CAMX_WAVES_F64 : RT_CAMX_WAVES)
 template <class R, class Trav, bool CAMX>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Trav::kWaves))) void k_persist_occ(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CAMX ? RT_CAMX_W(R) : Trav::kWaves))) void k_persist_occ(
     Params<R> p) {
   persist_body<R, Trav, CAMX>(p);
 }
@@ -1370,7 +1439,7 @@ __global__ __launch_bounds__(kBlock) void k_step(Params<R> p) {
   step_body<R, Trav, CAMX>(p);
 }
 template <class R, class Trav, bool CAMX>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Trav::kWaves))) void k_step_occ(Params<R> p) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CAMX ? RT_CAMX_W(R) : Trav::kWaves))) void k_step_occ(Params<R> p) {
   step_body<R, Trav, CAMX>(p);
 }
 
@@ -1750,29 +1819,33 @@ inline size_t wide_lds_bytes(const DevScene<R>& sc, bool ldsn) {
   return (ldsn ? (size_t)sc.n_wnodes * kWNodeLdsStride + (size_t)sc.n_wprim_words * sizeof(typename WWord<R>::T) : 0u) +
          stack;
 }
-template <class R, bool SPH, bool TRI, bool QUAD, bool MOV>
+template <class R, bool SPH, bool TRI, bool QUAD, bool MOV, bool LL = false, bool NL = false>
 void launch_wide_k(const Params<R>& p, uint32_t grid, hipStream_t st) {
   const size_t full = wide_lds_bytes(p.sc, true);
   const uint32_t spill_grid = p.sc.wide_spill ? std::min<uint32_t>(grid, p.sc.spill_lanes / kBlock) : grid;
   // LDS-resident trees use 16-bit child codes (wide_code16): node offset (index x 9) < 2^15, first word < 2^12
   if (full <= kWideLdsBudget && p.sc.n_wnodes * kWNodeLdsUnits < 0x8000u && p.sc.n_wprim_words <= 0x1000u) {
-    launch_one(k_persist_occ<R, WideTrav<R, SPH, TRI, QUAD, MOV, true>, false>, p, grid, st, full);
+    launch_one(k_persist_occ<R, WideTrav<R, SPH, TRI, QUAD, MOV, true, LL, NL>, false>, p, grid, st, full);
     return;
   }
   // the spill area holds spill_lanes lanes: never launch more (the resident grid is below it)
-  launch_one(k_persist_occ<R, WideTrav<R, SPH, TRI, QUAD, MOV, false>, false>, p, spill_grid, st,
+  launch_one(k_persist_occ<R, WideTrav<R, SPH, TRI, QUAD, MOV, false, LL, NL>, false>, p, spill_grid, st,
              wide_lds_bytes(p.sc, false));
 }
 // Kernel for the primitive kinds of the scene: spheres only (RTOW), triangles only or triangles and
 // quads (meshes, the C4 stand-in with its light), or all.
 template <class R>
-inline void launch_wide(const Params<R>& p, uint32_t grid, hipStream_t st) {
+inline void launch_wide(const Params<R>& p, bool ll, bool nl, uint32_t grid, hipStream_t st) {
   const uint32_t k = p.sc.wide_kinds;
-  if (k == WK_SPHERE)
+  if (k == WK_SPHERE && RT_WIDE_NL && nl)  // RTOW (C3)
+    launch_wide_k<R, true, false, false, false, false, true>(p, grid, st);
+  else if (k == WK_SPHERE)
     launch_wide_k<R, true, false, false, false>(p, grid, st);
   else if (k == WK_TRI)
     launch_wide_k<R, false, true, false, false>(p, grid, st);
-  else if (RT_WIDE_TRIQUAD && k == (WK_TRI | WK_QUAD))  // a mesh under a quad light (the C4 stand-in)
+  else if (RT_WIDE_TRIQUAD && k == (WK_TRI | WK_QUAD) && RT_WIDE_LL && ll && p.sc.n_mats <= 16)
+    launch_wide_k<R, false, true, true, false, true>(p, grid, st);  // ... lambertian + light (the C4 stand-in)
+  else if (RT_WIDE_TRIQUAD && k == (WK_TRI | WK_QUAD))  // a mesh under a quad light
     launch_wide_k<R, false, true, true, false>(p, grid, st);
   else
     launch_wide_k<R, true, true, true, true>(p, grid, st);
@@ -1780,18 +1853,23 @@ inline void launch_wide(const Params<R>& p, uint32_t grid, hipStream_t st) {
 template <class R, class Trav>
 void launch_k(const Params<R>& p, uint32_t grid, hipStream_t st) {
   const bool camx = p.cam_mode != RT_CAM_PERSPECTIVE || p.sc.has_procedural;
-  // the extended kernels run without the occupancy budget (their noise / camera code would spill)
+  // the flat program only runs perspective renders without procedural textures (kernel_family): no CAMX form
+  if (camx && !Trav::kFlat) {
+    if constexpr (!Trav::kFlat) {
+      if (p.persist)
+        launch_one(k_persist_occ<R, Trav, true>, p, grid, st);
+      else
+        launch_one(k_step_occ<R, Trav, true>, p, grid, st);
+    }
+    return;
+  }
   if (p.persist) {
-    if (camx)
-      launch_one(k_persist<R, Trav, true>, p, grid, st);
-    else if constexpr (Trav::kWaves > 1)
+    if constexpr (Trav::kWaves > 1)
       launch_one(k_persist_occ<R, Trav, false>, p, grid, st);
     else
       launch_one(k_persist<R, Trav, false>, p, grid, st);
   } else {
-    if (camx)
-      launch_one(k_step<R, Trav, true>, p, grid, st);
-    else if constexpr (Trav::kWaves > 1)
+    if constexpr (Trav::kWaves > 1)
       launch_one(k_step_occ<R, Trav, false>, p, grid, st);
     else
       launch_one(k_step<R, Trav, false>, p, grid, st);
@@ -1837,8 +1915,14 @@ bool lamb_light_scene(const SceneHeader& h) {
   return (h.mat_kinds & ~ok_m) == 0 && (h.tex_kinds & ~(1u << T_SOLID)) == 0 && h.light_kind == L_QUAD &&
          h.light_aligned != 0;
 }
+// no light, lambertian / metal / dielectric materials with solid or checker textures (RTOW): shade NL
+bool no_light_scene(const SceneHeader& h) {
+  const uint32_t ok_m = (1u << M_LAMBERTIAN) | (1u << M_METAL) | (1u << M_DIELECTRIC);
+  return (h.mat_kinds & ~ok_m) == 0 && (h.tex_kinds & ~((1u << T_SOLID) | (1u << T_CHECKER))) == 0 &&
+         h.light_kind == L_NONE;
+}
 template <class R>
-void launch_step(const Params<R>& p, KernelFamily fam, bool ll, int stack, uint32_t grid, hipStream_t st) {
+void launch_step(const Params<R>& p, KernelFamily fam, bool ll, bool nl, int stack, uint32_t grid, hipStream_t st) {
   switch (fam) {
     case KF_FLAT:
       if constexpr (family_built(KF_FLAT)) {
@@ -1865,7 +1949,7 @@ void launch_step(const Params<R>& p, KernelFamily fam, bool ll, int stack, uint3
       if constexpr (family_built(KF_LIN_ALL)) launch_k<R, LinearTrav<R, true, true, true>>(p, grid, st);
       return;
     case KF_WIDE:
-      if constexpr (family_built(KF_WIDE)) launch_wide(p, grid, st);
+      if constexpr (family_built(KF_WIDE)) launch_wide(p, ll, nl, grid, st);
       return;
     case KF_STACK:
       if constexpr (family_built(KF_STACK)) {
@@ -1981,7 +2065,7 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     const KernelFamily fam = kernel_family(hdr, cam->mode, persist, prm->traversal == RT_TRAV_ORDERED);
     if (!family_built(fam))
       return set_err(c, RT_ERR_UNSUPPORTED, std::string("this build (RT_DEV_ONLY) has no ") + family_name(fam) + " kernels");
-    const bool ll = lamb_light_scene(hdr);
+    const bool ll = lamb_light_scene(hdr), nl = no_light_scene(hdr);
     uint32_t P = prm->pool_slots > 0 ? (uint32_t)prm->pool_slots
                  : persist       ? kAutoPersistLanes
                                  : (f64 ? kAutoPool64 : kAutoPool32);
@@ -2088,11 +2172,11 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
           hipEvent_t e0 = take_event(c, ev0 + ev), e1 = take_event(c, ev0 + ev + 1);
           if (!e0 || !e1) return set_err(c, RT_ERR_HIP, "hipEventCreate failed");
           RT_HIP(c, hipEventRecord(e0, st));
-          launch_step<R>(p, fam, ll, cs.stack_need, grid, st);
+          launch_step<R>(p, fam, ll, nl, cs.stack_need, grid, st);
           RT_HIP(c, hipEventRecord(e1, st));
           ev += 2;
         } else {
-          launch_step<R>(p, fam, ll, cs.stack_need, grid, st);
+          launch_step<R>(p, fam, ll, nl, cs.stack_need, grid, st);
         }
         RT_HIP(c, hipGetLastError());
         c->last.grid_lanes = t_grid_lanes;
@@ -2122,11 +2206,11 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
               hipEvent_t e0 = take_event(c, ev0 + ev), e1 = take_event(c, ev0 + ev + 1);
               if (!e0 || !e1) return set_err(c, RT_ERR_HIP, "hipEventCreate failed");
               RT_HIP(c, hipEventRecord(e0, st));
-              launch_step<R>(p, fam, ll, cs.stack_need, grid, st);
+              launch_step<R>(p, fam, ll, nl, cs.stack_need, grid, st);
               RT_HIP(c, hipEventRecord(e1, st));
               ev += 2;
             } else {
-              launch_step<R>(p, fam, ll, cs.stack_need, grid, st);
+              launch_step<R>(p, fam, ll, nl, cs.stack_need, grid, st);
             }
             launches++;
             iters++;
@@ -2371,6 +2455,12 @@ rt_status rt_set_timing(rt_context* c, int32_t enable) {
   return RT_OK;
 }
 
+#ifdef RT_ITEM_CLOCKS
+// development build only (scripts/dev_item_clocks.py): where the persistent kernels write item durations
+int rt_dev_set_item_clocks(void* dev_ptr) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_item_clk), &dev_ptr, sizeof(void*)) == hipSuccess ? 0 : -1;
+}
+#endif
 #ifdef RT_SECTION_CLOCKS
 // development build only (scripts/dev_sections.py): read and clear the section clocks
 int rt_dev_section_clocks(unsigned long long out[7]) {
