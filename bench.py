@@ -284,6 +284,41 @@ def parity_tiles(fb, W, tiles, ref, rel_tol=None):
     return out
 
 
+class Hip:
+    """The few HIP runtime calls bench.py's copy stream needs, through ctypes (libamdhip64 is loaded by torch)."""
+
+    def __init__(self):
+        import ctypes
+        self.ct = ctypes
+        self.lib = ctypes.CDLL("libamdhip64.so")
+        for name, args in (("hipEventCreateWithFlags", [ctypes.c_void_p, ctypes.c_uint]),
+                           ("hipEventRecord", [ctypes.c_void_p, ctypes.c_void_p]),
+                           ("hipStreamWaitEvent", [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]),
+                           ("hipMemcpyAsync", [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                               ctypes.c_void_p])):
+            getattr(self.lib, name).argtypes = args
+            getattr(self.lib, name).restype = ctypes.c_int
+
+    def _ok(self, e, what):
+        if e != 0:
+            raise RuntimeError(f"{what} failed: hip error {e}")
+
+    def event(self):
+        ev = self.ct.c_void_p()
+        self._ok(self.lib.hipEventCreateWithFlags(self.ct.byref(ev), 2), "hipEventCreateWithFlags")  # no timing
+        return ev
+
+    def record(self, ev, stream):
+        self._ok(self.lib.hipEventRecord(ev, self.ct.c_void_p(stream)), "hipEventRecord")
+
+    def wait(self, stream, ev):
+        self._ok(self.lib.hipStreamWaitEvent(self.ct.c_void_p(stream), ev, 0), "hipStreamWaitEvent")
+
+    def d2h(self, dst, src, nbytes, stream):
+        self._ok(self.lib.hipMemcpyAsync(self.ct.c_void_p(dst), self.ct.c_void_p(src), nbytes, 2,
+                                         self.ct.c_void_p(stream)), "hipMemcpyAsync")
+
+
 def measured_pmc(workload):
     """Per-launch PMC figures of the dominant kernel for this exact workload and build (profiles/*_pmc.json,
     written by scripts/pmc_summary.py from separate rocprofv3 --pmc passes; the last in name order wins),
@@ -447,6 +482,8 @@ def main():
     counts = shard.counts
 
     copy_stream = torch.cuda.Stream(dev)
+    copy_h = copy_stream.cuda_stream
+    hip = Hip()
 
     def run(precision, steps, warmup, timing):
         """warmup + `steps` timed frames; returns (elapsed s (max over ranks), stats, rank 0's host framebuffer
@@ -461,26 +498,29 @@ def main():
         # renders, so only the last frame's copy is exposed; a buffer's next scatter waits for its last copy.
         fbs = [fb, torch.zeros_like(fb)] if rank == 0 else [None, None]
         hosts = [torch.empty(fb.shape, dtype=tdtype, pin_memory=True) for _ in range(2)] if rank == 0 else None
-        copied = [None, None]
         nstep = [0]
+        # the copies and their ordering by HIP calls (events made once): torch's per-call event and stream
+        # objects cost ~1 ms of host time per frame, more than C1's whole 0.6 ms frame
+        cur_h = torch.cuda.current_stream(dev).cuda_stream
+        ready = [hip.event() for _ in range(2)]
+        copied = [hip.event() for _ in range(2)]
+        used = [False, False]
+        nbytes = fb.numel() * fb.element_size() if rank == 0 else 0
 
         def step():
             k = nstep[0] % 2
             nstep[0] += 1
-            cur = torch.cuda.current_stream(dev)
-            if copied[k] is not None:
-                cur.wait_event(copied[k])
+            if used[k]:
+                hip.wait(cur_h, copied[k])
             # render this rank's tiles on torch's current stream (the default = the HIP null stream); the
             # RCCL gather and rank 0's scatter are queued behind it on the same stream
             shard.frame(ctx, cam, params, out, fbs[k])
             if rank == 0:
-                ready = torch.cuda.Event()
-                ready.record(cur)
-                copy_stream.wait_event(ready)
-                with torch.cuda.stream(copy_stream):
-                    hosts[k].copy_(fbs[k], non_blocking=True)
-                    copied[k] = torch.cuda.Event()
-                    copied[k].record(copy_stream)
+                hip.record(ready[k], cur_h)
+                hip.wait(copy_h, ready[k])
+                hip.d2h(hosts[k].data_ptr(), fbs[k].data_ptr(), nbytes, copy_h)
+                hip.record(copied[k], copy_h)
+                used[k] = True
 
         for _ in range(warmup):
             step()

@@ -403,16 +403,38 @@ struct DevScene {
   uint32_t n_wnodes, n_wprim_words, wroot, wide_stack, wide_kinds;
   int32_t has_wide;
   uint32_t wide_big;  // primitives at the head of the word stream, tested before the tree
+  uint32_t wide_top;  // nodes [0, wide_top): the tree's first levels (HBM trees: read from an LDS copy)
   const WNodeH* wnodesh;  // the fp16 form of the tree (rt_scene.h WNodeH; 0: none)
-  // a tree in HBM keeps at most kWideLdsStack stack entries per lane in LDS; deeper entries (rare:
-  // every child of every node on a path hit) go to wide_spill[(depth - kWideLdsStack) * spill_lanes + lane]
+  // a tree in HBM keeps at most wide_lds_stack<R>() stack entries per lane in LDS; deeper entries go to
+  // wide_spill[(depth - wide_lds_stack<R>()) * spill_lanes + lane]
   uint32_t* wide_spill;
   uint32_t spill_lanes;
 };
-#ifndef RT_WIDE_LDS_STACK
-#define RT_WIDE_LDS_STACK 24
+#ifndef RT_WIDE_TOP  // fp32 rays over trees in HBM: the tree's first levels read from LDS (trace_wide)
+#define RT_WIDE_TOP 1
 #endif
-constexpr uint32_t kWideLdsStack = RT_WIDE_LDS_STACK;
+#ifndef RT_WIDE_TOP_N  // at most this many of them (the builder orders up to kWideTopMax breadth-first)
+#define RT_WIDE_TOP_N 55
+#endif
+#ifndef RT_WIDE_TOP_F64  // the same for fp64 rays, whose HBM trees are read in the fp16 form (WNodeH)
+#define RT_WIDE_TOP_F64 1
+#endif
+#ifndef RT_WIDE_TOP_N_F64
+#define RT_WIDE_TOP_N_F64 85
+#endif
+#ifndef RT_WIDE_LDS_STACK
+#define RT_WIDE_LDS_STACK 12
+#endif
+#ifndef RT_WIDE_LDS_STACK_F64
+#define RT_WIDE_LDS_STACK_F64 24
+#endif
+// stack entries per lane kept in LDS for a tree in HBM, by ray precision (fp32: fewer, so the LDS also holds
+// the top of the tree and 8 blocks fit a CU; C4 fp32, stack / top nodes / waves: 24 / 0 / 6 309.4 ms/frame,
+// 22 / 21 / 6 290.1, 16 / 47 / 7 268.8, 14 / 63 / 7 268.1, 12 / 55 / 8 265.2; r05r-r05u)
+template <class R>
+constexpr uint32_t wide_lds_stack() {
+  return sizeof(R) == 4 ? RT_WIDE_LDS_STACK : RT_WIDE_LDS_STACK_F64;
+}
 
 // World -> object through an instance chain (hittable.h:75-82, 125-135, 192-202, 259-270).
 template <class R>
@@ -1115,7 +1137,8 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
   int sp = ry.sp;
   R tmax = ry.tmax;
   uint32_t e_best = ry.e;
-  // the lane's stack: LDS, and for a tree in HBM its spill area past kWideLdsStack entries
+  // the lane's stack: LDS, and for a tree in HBM its spill area past wide_lds_stack<R>() entries
+  constexpr uint32_t kWideLdsStack = wide_lds_stack<R>();
   [[maybe_unused]] const uint32_t lane = blockIdx.x * BLOCK + threadIdx.x;
   auto push = [&](uint32_t v) {
     if (LDSN || sp < (int)kWideLdsStack)
@@ -1191,7 +1214,14 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
   const unsigned char* nbase = LDSN ? lds_nodes : (const unsigned char*)sc.wnodes;
   using OfsT = typename std::conditional<kOfs, uint32_t, uint64_t>::type;
   auto node_off = [](uint32_t c) -> OfsT { return LDSN ? (OfsT)(c << 4) : (OfsT)c * (OfsT)sizeof(WNode); };
-  auto node_keys = [&](OfsT nof, uint32_t& k0, uint32_t& k1, uint32_t& k2, uint32_t& k3) {
+  // a node's 16-byte rows: from the tree's memory, or (RT_WIDE_TOP) from the LDS copy of its first levels
+  auto ld_mem = [&](OfsT off) -> float4 { return *(const float4*)(nbase + off); };
+  using LdsF = const __attribute__((address_space(3))) float;
+  [[maybe_unused]] auto ld_top = [&](OfsT off) -> float4 {
+    LdsF* q = (LdsF*)(lds_nodes + off);
+    return make_float4(q[0], q[1], q[2], q[3]);
+  };
+  auto node_keys_from = [&](auto ld4, OfsT nof, uint32_t& k0, uint32_t& k1, uint32_t& k2, uint32_t& k3) {
     const float tmx = (float)tmax;
     // tn >= tmin > 0: the bit pattern orders like the value; the low 2 bits carry the slot
     auto keyof = [](float tn, float tf, uint32_t c) {
@@ -1205,10 +1235,8 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
         ony = (oct >> 8) & 0xFFu;
         onz = oct >> 16;
       }
-      const float4 nx = *(const float4*)(nbase + (nof + onx)), ny = *(const float4*)(nbase + (nof + ony)),
-                   nz = *(const float4*)(nbase + (nof + onz));
-      const float4 fx = *(const float4*)(nbase + (nof + (48u - onx))), fy = *(const float4*)(nbase + (nof + (80u - ony))),
-                   fz = *(const float4*)(nbase + (nof + (112u - onz)));
+      const float4 nx = ld4(nof + onx), ny = ld4(nof + ony), nz = ld4(nof + onz);
+      const float4 fx = ld4(nof + (48u - onx)), fy = ld4(nof + (80u - ony)), fz = ld4(nof + (112u - onz));
       auto key = [&](float px, float py, float pz, float qx, float qy, float qz, uint32_t c) {
         float tn, tf;
         if constexpr (kFma) {
@@ -1251,6 +1279,14 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
       k3 = slab(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, 3u);
     }
   };
+  auto node_keys = [&](OfsT nof, uint32_t& k0, uint32_t& k1, uint32_t& k2, uint32_t& k3) {
+    node_keys_from(ld_mem, nof, k0, k1, k2, k3);
+  };
+  // RT_WIDE_TOP (fp32 rays over a tree in HBM): nodes [0, wide_top) -- the first levels, which every ray
+  // visits -- are read from the LDS copy the kernel made at its start (WideTrav::fill), so those visits
+  // take no slot of the L1 address path, the C4 kernel's bound
+  constexpr bool kTopL = !LDSN && !F64 && RT_WIDE_TOP;
+  [[maybe_unused]] const uint32_t ntop = kTopL ? min(sc.wide_top, (uint32_t)RT_WIDE_TOP_N) : 0u;
   // RT_WIDE_HALF_F64: the keys of node c from the tree's fp16 form (rt_scene.h WNodeH), and its child codes.
   // A plane's distance is one fma of its fp16 offset (v_fma_mix_f32): h * inv + b, b = (origin - o) *
   // inv per node and axis. b carries two roundings, |b| 2^-23 at most: the near planes take b - e and
@@ -1263,11 +1299,19 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
   [[maybe_unused]] const uint32_t selx = (__float_as_uint(inv.x) >> 31) ? 0x07060504u : 0x03020100u,
                                   sely = (__float_as_uint(inv.y) >> 31) ? 0x07060504u : 0x03020100u,
                                   selz = (__float_as_uint(inv.z) >> 31) ? 0x07060504u : 0x03020100u;
-  [[maybe_unused]] auto half_keys = [&](uint32_t c, uint32_t& k0, uint32_t& k1, uint32_t& k2, uint32_t& k3, uint4& cc) {
-    const unsigned char* hp = hbase + c * (uint32_t)sizeof(WNodeH);
-    const uint4 h0 = *(const uint4*)hp;
-    uint4 h1 = *(const uint4*)(hp + 16), h2 = *(const uint4*)(hp + 32), h3 = *(const uint4*)(hp + 48);
-    cc = *(const uint4*)(hp + 64);
+  // the node's 16-byte words from the tree in HBM, or (RT_WIDE_TOP_F64) from the LDS copy of its first levels
+  [[maybe_unused]] auto ldh_mem = [&](uint32_t off) -> uint4 { return *(const uint4*)(hbase + off); };
+  using LdsU = const __attribute__((address_space(3))) uint32_t;
+  [[maybe_unused]] auto ldh_top = [&](uint32_t off) -> uint4 {
+    LdsU* q = (LdsU*)(lds_nodes + off);
+    return make_uint4(q[0], q[1], q[2], q[3]);
+  };
+  [[maybe_unused]] auto half_keys_from = [&](auto ld16, uint32_t c, uint32_t& k0, uint32_t& k1, uint32_t& k2,
+                                             uint32_t& k3, uint4& cc) {
+    const uint32_t hp = c * (uint32_t)sizeof(WNodeH);
+    const uint4 h0 = ld16(hp);
+    uint4 h1 = ld16(hp + 16), h2 = ld16(hp + 32), h3 = ld16(hp + 48);
+    cc = ld16(hp + 64);
     {  // lo: x h1.xy, y h1.zw, z h2.xy; hi: x h2.zw, y h3.xy, z h3.zw -> near in the lo words, far in the hi
       auto pick = [](uint32_t& lo, uint32_t& hi, uint32_t sel) {
         const uint32_t n = __builtin_amdgcn_perm(hi, lo, sel), f = __builtin_amdgcn_perm(lo, hi, sel);
@@ -1352,6 +1396,11 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
       }
     }
   };
+  [[maybe_unused]] auto half_keys = [&](uint32_t c, uint32_t& k0, uint32_t& k1, uint32_t& k2, uint32_t& k3, uint4& cc) {
+    half_keys_from(ldh_mem, c, k0, k1, k2, k3, cc);
+  };
+  constexpr bool kTopH = kHalf && RT_WIDE_TOP_F64;
+  [[maybe_unused]] const uint32_t ntoph = kTopH ? min(sc.wide_top, (uint32_t)RT_WIDE_TOP_N_F64) : 0u;
   if (ry.fresh) {  // every lane alike: no divergence, and the tree starts bounded by their hit
     test_prims(0u, sc.wide_big);
     ry.fresh = 0;
@@ -1390,8 +1439,23 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
         uint4 cc{};
         uint32_t k0, k1, k2, k3;
         [[maybe_unused]] OfsT nof{};
-        if constexpr (kHalf) {
+        if constexpr (kTopH) {
+          if (cur < ntoph)
+            half_keys_from(ldh_top, cur, k0, k1, k2, k3, cc);
+          else
+            half_keys(cur, k0, k1, k2, k3, cc);
+        } else if constexpr (kHalf) {
           half_keys(cur, k0, k1, k2, k3, cc);
+        } else if constexpr (kTopL) {
+          nof = node_off(cur);
+          if (cur < ntop) {
+            const float4 c4 = ld_top(nof + 96u);
+            cc = make_uint4(__float_as_uint(c4.x), __float_as_uint(c4.y), __float_as_uint(c4.z), __float_as_uint(c4.w));
+            node_keys_from(ld_top, nof, k0, k1, k2, k3);
+          } else {
+            cc = *(const uint4*)(nbase + (nof + 96u));
+            node_keys(nof, k0, k1, k2, k3);
+          }
         } else {
           nof = node_off(cur);
           if constexpr (!LDSN) cc = *(const uint4*)(nbase + (nof + 96u));

@@ -1041,7 +1041,7 @@ struct StackTrav {
 #endif
 #ifndef RT_WIDE_WAVES_GLOBAL  // tree in HBM, 32-bit stack in LDS (C4 stand-in: 4 waves 519 ms, 5: 462; with the
 // speculative traversal 5: 424, 6: 412.5 -- 7 blocks of 24 KB stacks do not fit the 160 KB LDS)
-#define RT_WIDE_WAVES_GLOBAL 6
+#define RT_WIDE_WAVES_GLOBAL 8  // round 5, with 12 LDS stack entries and 55 top nodes in LDS (wide_lds_stack)
 #endif
 #ifndef RT_WIDE_TRIQUAD  // a kernel for triangle + quad scenes (else the all-kinds kernel): C4 358.9 -> 353.8 ms
 #define RT_WIDE_TRIQUAD 1
@@ -1068,7 +1068,7 @@ struct StackTrav {
 #define RT_WIDE_WAVES_GLOBAL_F64_LL 5  // (r05g; the general kernel at 4: 526.7)
 #endif
 #ifndef RT_WIDE_WAVES_F64_NL  // the NL form over an LDS tree, fp64 (116 VGPRs at 4 waves)
-#define RT_WIDE_WAVES_F64_NL 4
+#define RT_WIDE_WAVES_F64_NL 5  // C3 fp64 at 4 waves 69.07 ms/frame, 5: 65.41 (r05q; the general kernel at 4: 70.23)
 #endif
 #ifndef RT_WIDE_NL  // a wide kernel for sphere scenes without a light (shade NL)
 #define RT_WIDE_NL 1
@@ -1103,6 +1103,12 @@ struct WideTrav {
   __host__ __device__ static uint32_t stack_offset(uint32_t n_wnodes, uint32_t n_words) {
     return LDSN ? n_wnodes * kWNodeLdsStride + n_words * (uint32_t)sizeof(WW) : 0u;
   }
+  // a tree in HBM, fp32 rays (RT_WIDE_TOP): [stack][the first wide_top nodes, WNode layout]
+  static constexpr bool kTop = !LDSN && sizeof(R) == 4 && RT_WIDE_TOP;
+  static constexpr bool kTopH = !LDSN && sizeof(R) == 8 && RT_WIDE_HALF_F64 && RT_WIDE_TOP_F64;
+  __host__ __device__ static uint32_t top_offset(uint32_t wide_stack) {
+    return (wide_stack < wide_lds_stack<R>() ? wide_stack : wide_lds_stack<R>()) * kBlock * 4u;
+  }
   __host__ __device__ static uint32_t root(const DevScene<R>& sc) {
     return LDSN ? wide_code16(sc.wroot) : sc.wroot;
   }
@@ -1123,6 +1129,19 @@ struct WideTrav {
       for (uint32_t j = threadIdx.x; j < n16; j += kBlock) pw[j] = gp[j];
       __syncthreads();
     }
+    if constexpr (kTop) {
+      uint4* dst = (uint4*)(base + top_offset(sc.wide_stack));
+      const uint4* gn = (const uint4*)sc.wnodes;
+      const uint32_t ntop = min(sc.wide_top, (uint32_t)RT_WIDE_TOP_N);
+      for (uint32_t j = threadIdx.x; j < ntop * 8u; j += kBlock) dst[j] = gn[j];
+      __syncthreads();
+    } else if constexpr (kTopH) {  // fp64 rays: the fp16 form, 5 words per node
+      uint4* dst = (uint4*)(base + top_offset(sc.wide_stack));
+      const uint4* gn = (const uint4*)sc.wnodesh;
+      const uint32_t ntop = min(sc.wide_top, (uint32_t)RT_WIDE_TOP_N_F64);
+      for (uint32_t j = threadIdx.x; j < ntop * 5u; j += kBlock) dst[j] = gn[j];
+      __syncthreads();
+    }
     return (StackT*)(base + stack_offset(sc.n_wnodes, sc.n_wprim_words));
   }
   // Advance the ray of s (false: paused, see trace_wide)
@@ -1130,8 +1149,10 @@ struct WideTrav {
   __device__ __forceinline__ static bool steps(const DevScene<R>& sc, const Node<R>* lds, const PS& s, StackT* stk,
                                                WideRayT<R>& ry) {
     const unsigned char* base = (const unsigned char*)lds;
+    // LDSN: the whole tree at the base; kTop: the copy of the tree's first levels after the stack
     return trace_wide<R, SPH, TRI, QUAD, MOV, LDSN, kBlock, LDSN ? RT_SHADE_BATCH : RT_SHADE_BATCH_GLOBAL>(
-        sc, base, (const WW*)(base + sc.n_wnodes * kWNodeLdsStride), s.o, s.d, s.tm, s.xe, stk, ry);
+        sc, (kTop || kTopH) ? base + top_offset(sc.wide_stack) : base, (const WW*)(base + sc.n_wnodes * kWNodeLdsStride), s.o,
+        s.d, s.tm, s.xe, stk, ry);
   }
 };
 
@@ -1614,7 +1635,7 @@ struct rt_context {
   bool has_scene = false;
   DevBuf scene32, scene64;
   DevBuf state, partial, pixmap, queue0, queue1, blk, out_tmp, counters, camx, heads, tiles;
-  DevBuf wide_spill;  // the wide traversal's stack entries past kWideLdsStack (deep trees in HBM)
+  DevBuf wide_spill;  // the wide traversal's stack entries past wide_lds_stack (deep trees in HBM)
   CamDev cam_host;  // source of camx (kept alive for the async copy)
   uint32_t* total_host = nullptr;  // pinned: [0] live slots, [1] fault word, [16..] segment counter shards
   uint64_t samples = 0;
@@ -1767,6 +1788,7 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
   s.wide_stack = h.wide_stack;
   s.wide_kinds = h.wide_kinds;
   s.wide_big = h.wide_big;
+  s.wide_top = h.wide_top;
   s.wnodesh = h.has_wnodesh ? (const WNodeH*)at(h.off_wnodesh) : nullptr;
   return s;
 }
@@ -1813,11 +1835,16 @@ void launch_one(KernelT kern, Params<R> p, uint32_t grid, hipStream_t st, size_t
 constexpr size_t kWideLdsBudget = 40u << 10;  // bytes per 256-lane block: 4 blocks per CU of 160 KiB
 template <class R>
 inline size_t wide_lds_bytes(const DevScene<R>& sc, bool ldsn) {
-  // an LDS tree: every entry in LDS, uint16; a tree in HBM: up to kWideLdsStack uint32 entries (the rest spill)
+  // an LDS tree: every entry in LDS, uint16; a tree in HBM: up to wide_lds_stack uint32 entries (the rest spill)
   const size_t stack = ldsn ? (size_t)sc.wide_stack * kBlock * 2u
-                            : (size_t)std::min<uint32_t>(sc.wide_stack, kWideLdsStack) * kBlock * 4u;
+                            : (size_t)std::min<uint32_t>(sc.wide_stack, wide_lds_stack<R>()) * kBlock * 4u;
+  // fp32 rays over a tree in HBM: the copy of its first levels (RT_WIDE_TOP)
+  const size_t top = (!ldsn && sizeof(R) == 4 && RT_WIDE_TOP)
+                         ? (size_t)std::min<uint32_t>(sc.wide_top, RT_WIDE_TOP_N) * sizeof(WNode)
+                     : (!ldsn && sizeof(R) == 8 && RT_WIDE_HALF_F64 && RT_WIDE_TOP_F64)
+                         ? (size_t)std::min<uint32_t>(sc.wide_top, RT_WIDE_TOP_N_F64) * sizeof(WNodeH) : 0u;
   return (ldsn ? (size_t)sc.n_wnodes * kWNodeLdsStride + (size_t)sc.n_wprim_words * sizeof(typename WWord<R>::T) : 0u) +
-         stack;
+         stack + top;
 }
 template <class R, bool SPH, bool TRI, bool QUAD, bool MOV, bool LL = false, bool NL = false>
 void launch_wide_k(const Params<R>& p, uint32_t grid, hipStream_t st) {
@@ -2104,6 +2131,7 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     Params<R> p{};
     p.sc = dev_scene<R>(hdr, sbase);
     const uint32_t wide_need = hdr.wide_stack;
+    constexpr uint32_t kWideLdsStack = wide_lds_stack<R>();
     if (hdr.has_wide && wide_need > kWideLdsStack) {
       // a deep wide tree: a spill area of (need - kWideLdsStack) entries for every lane the chip can hold
       int ncu = 0;

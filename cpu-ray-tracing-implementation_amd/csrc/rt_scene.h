@@ -231,6 +231,9 @@ constexpr uint32_t kWFirstMask = (1u << kWCountShift) - 1u;
 constexpr int kWLeafMax = 3;         // primitives per leaf (triangles, mixed kinds)
 constexpr int kWLeafMaxSpheres = 6;  // sphere-only trees (at most 8: the LDS code's 3-bit count)
 constexpr int kWideStackMax = 96;  // stack entries a ray may need in the wide tree (beyond LDS: a spill area)
+// top-of-tree nodes ordered first, breadth-first (three levels of a 4-wide tree); the HBM kernels copy the
+// first RT_WIDE_TOP_N of them to LDS
+constexpr uint32_t kWideTopMax = 85;
 // primitive kinds present (SceneHeader::wide_kinds)
 enum : uint32_t { WK_SPHERE = 1u, WK_TRI = 2u, WK_QUAD = 4u, WK_MOVING = 8u };
 
@@ -314,6 +317,7 @@ struct SceneHeader {
   uint32_t tex_kinds;   // bit T_* of every material's texture kind (the background's too)
   int32_t light_kind;   // L_* of the importance-sampling light
   int32_t light_aligned;
+  uint32_t wide_top;    // the wide tree's first levels, breadth-first: nodes [0, wide_top) (LDS copy, HBM trees)
 };
 
 }  // namespace rtd

@@ -1329,6 +1329,39 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
   uint32_t root;
   int need;
   const bool ok = emit(0, root, need);
+  // The top of the tree first (round 5): the nodes of the first levels, in breadth-first order, take
+  // indices [0, top) -- kernels over a tree in HBM keep them in LDS (every ray visits them) -- and the rest
+  // keep their depth-first order (subtrees contiguous). The deepest level that fits kWideTopMax nodes.
+  uint32_t top = 0;
+  if (ok && !(root & kWLeaf) && wn.size() > 1) {
+    std::vector<uint32_t> bfs{root}, level{root};
+    std::vector<uint32_t> chosen;
+    for (int depth = 0; depth < 8 && !level.empty(); depth++) {
+      if (bfs.size() > kWideTopMax) break;
+      chosen = bfs;
+      std::vector<uint32_t> next;
+      for (uint32_t n : level)
+        for (int c = 0; c < 4; c++)
+          if (!(wn[n].child[c] & kWLeaf)) next.push_back(wn[n].child[c]);
+      bfs.insert(bfs.end(), next.begin(), next.end());
+      level.swap(next);
+    }
+    top = (uint32_t)chosen.size();
+    std::vector<uint32_t> perm(wn.size(), 0xFFFFFFFFu);
+    uint32_t k = 0;
+    for (uint32_t n : chosen) perm[n] = k++;
+    for (uint32_t n = 0; n < wn.size(); n++)
+      if (perm[n] == 0xFFFFFFFFu) perm[n] = k++;
+    std::vector<WNode> re(wn.size());
+    for (uint32_t n = 0; n < wn.size(); n++) {
+      WNode w = wn[n];
+      for (int c = 0; c < 4; c++)
+        if (!(w.child[c] & kWLeaf)) w.child[c] = perm[w.child[c]];
+      re[perm[n]] = w;
+    }
+    wn.swap(re);
+    root = perm[root];
+  }
   if (std::getenv("RT_DEBUG_WIDE"))
     std::fprintf(stderr, "[wide] ok %d need %d nodes %zu words %zu binary nodes %zu\n", (int)ok, need, wn.size(),
                  words.size(), bn.size());
@@ -1361,6 +1394,7 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
     h.wide_stack = (uint32_t)std::max(1, need);
     h.wide_kinds = kinds;
     h.wide_big = (uint32_t)big.size();
+    h.wide_top = top;
     h.has_wide = 1;
   }
   SceneHeader& h = out->hdr;
@@ -1375,6 +1409,7 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
   h.wide_stack = (uint32_t)std::max(1, need);
   h.wide_kinds = kinds;
   h.wide_big = (uint32_t)big.size();
+  h.wide_top = top;
   h.has_wide = 1;
   return true;
 }
