@@ -83,6 +83,12 @@ constexpr int kBlock = 256;
                              // 128 VGPRs) 1661 ms/frame, 5: 1567, 6: 2594 (spills); round 4 (cold state in LDS,
 #define RT_LINEAR_VOL_WAVES 6  // radiance folded, table sin/cos): 5: 1,326, 6: 1,247
 #endif
+#ifndef RT_LIN_LLI  // the volume program for lambertian + isotropic + light scenes (shade LL, LLI): C5 fp32
+#define RT_LIN_LLI 1  // 1,189 -> 1,124 ms/frame, fp64 2,358 -> 2,262 (r05y)
+#endif
+#ifndef RT_LINEAR_VOL_WAVES_LLI  // its fp32 form at 7 waves (79 VGPRs at 6): 1,124 -> 1,097 ms/frame (r05y)
+#define RT_LINEAR_VOL_WAVES_LLI 7
+#endif
 #ifndef RT_LINEAR_VOL_WAVES_F64  // the fp64 volume program (round 4, cold state in LDS): 3 waves 2,672 ms/frame, 4: 2,400
 #define RT_LINEAR_VOL_WAVES_F64 4
 #endif
@@ -589,8 +595,9 @@ __global__ __launch_bounds__(kBlock) void k_init(Params<R> p) {
 // NL ("no light", round 5): the materials are lambertian, metal and dielectric (solid and checker textures)
 // and there is no importance-sampling light (RTOW, C3; host-checked): the emission, gloss, isotropic and
 // light-mixture code is compiled out.
+// LLI (with LL): isotropic phase materials too (the lm record's w is 2; C5's smoke volumes)
 template <class R, bool CAMX, bool FLAT = false, bool MOVING = true, bool MLDS = false, bool LL = false,
-          bool NL = false, class PS>
+          bool NL = false, bool LLI = false, class PS>
 __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, uint32_t nm = 0,
                       const Material<R>* mats = nullptr, const R4<R>* lm = nullptr) {
   const DevScene<R>& sc = p.sc;
@@ -737,10 +744,13 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
     const Material<R>& m = MLDS ? *(const Material<R>*)((LMat*)mats + mat) : sc.mats[mat];
     V<R> col{};
     bool is_light;
+    [[maybe_unused]] bool ll_iso = false;
     if constexpr (LL) {
       LRec* mc = (LRec*)lm + mat;
       col = mkv(mc->x, mc->y, mc->z);
-      is_light = mc->w != R(0);
+      const R w = mc->w;
+      is_light = w == R(1);
+      if constexpr (LLI) ll_iso = w == R(2);
     } else {
       is_light = !NL && m.kind == M_DIFFUSE_LIGHT;
     }
@@ -786,7 +796,7 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
         new_d = unit((R(1) - tt) * diffuse + tt * reflect(d, n));
       } else {  // lambertian (material.h:62-72) / isotropic (material.h:193-200) / gloss diffuse: kRandom
         if (!LL && !NL && m.kind == M_GLOSS) js++;  // the specular-choice draw above (material.h:161)
-        const bool iso = !LL && !NL && m.kind == M_ISOTROPIC;
+        const bool iso = LL ? (LLI && ll_iso) : (!NL && m.kind == M_ISOTROPIC);
         const R iso_pdf = R(1) / (R(4) * Num<R>::pi());
         Onb<R> b;
         if (!FLAT && !iso) b = make_onb(n);
@@ -913,14 +923,18 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
 // Each launch advances every live slot by up to K segments: closest hit
 // (extend, camera.h:198), then shade. Traversal: the wave-uniform linear
 // program (small scenes) or the BVH stack machine with a per-lane LDS stack.
-template <class R, bool SPH, bool TRI, bool VOL>
+// LLI: a lambertian + isotropic + light scene (shade LL, LLI; C5's Cornell box with smoke volumes)
+template <class R, bool SPH, bool TRI, bool VOL, bool LLI = false>
 struct LinearTrav {
+  static constexpr bool kLL = LLI;
+  static constexpr bool kLinLL = LLI;
+  static constexpr uint32_t kLdsMats = 16;
   static constexpr int kStack = 0;
   // waves per SIMD the register budget is cut for (occupancy hides the shading loads); the
   // lean quad-only program fits 96 VGPRs with a small spill, the others would spill heavily
   static constexpr int kWaves = sizeof(R) != 4 ? (VOL ? RT_LINEAR_VOL_WAVES_F64 : RT_LINEAR_WAVES_F64)
                                  : (!SPH && !TRI && !VOL) ? RT_LINEAR_WAVES
-                                 : (!SPH && !TRI && VOL)  ? RT_LINEAR_VOL_WAVES
+                                 : (!SPH && !TRI && VOL)  ? (LLI ? RT_LINEAR_VOL_WAVES_LLI : RT_LINEAR_VOL_WAVES)
                                                           : 1;
   static constexpr int kLdsNodes = 0;
   static constexpr bool kFlat = false;
@@ -960,6 +974,7 @@ struct LinearTrav {
 #endif
 template <class R, bool TLDS = false, bool LL = false>
 struct FlatTrav {
+  static constexpr bool kLinLL = false;
   static constexpr bool kTablesLds = TLDS;  // persistent kernel: Tables in LDS (fill, run_lds)
   static constexpr bool kLL = LL;           // lambertian + light scene (shade LL; the lm table)
   static constexpr int kStack = 0;
@@ -1015,6 +1030,7 @@ struct FlatTrav {
 constexpr uint32_t kLdsNodeMax = 256;
 template <class R, int STACK, bool LDSN = false>
 struct StackTrav {
+  static constexpr bool kLL = false, kLinLL = false;
   static constexpr int kStack = STACK;
   static constexpr int kLdsNodes = LDSN ? (int)kLdsNodeMax : 0;
   static constexpr int kWaves = sizeof(R) == 4 ? RT_STACK_WAVES : (LDSN ? 1 : RT_STACK_WAVES_F64);  // occupancy over a small spill
@@ -1083,6 +1099,7 @@ struct StackTrav {
 template <class R, bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN, bool LL = false, bool NL = false>
 struct WideTrav {
   static constexpr bool kLL = LL;
+  static constexpr bool kLinLL = false;
   static constexpr bool kNL = NL;  // no light (shade NL)
   static constexpr uint32_t kLdsMats = 16;
   static constexpr int kStack = 0;
@@ -1280,14 +1297,16 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
     __syncthreads();
     flat_tb = &tb;
   }
-  // the wide LL kernels: the materials as (colour, is_light) records in LDS (shade LL)
+  // the wide and linear LL kernels: the materials as (colour, kind) records in LDS, kind 0 lambertian, 1
+  // diffuse_light, 2 isotropic (shade LL, LLI)
   [[maybe_unused]] const R4<R>* wlm = nullptr;
-  if constexpr (Trav::kWide) {
+  if constexpr (Trav::kWide || Trav::kLinLL) {
     if constexpr (Trav::kLL) {
       __shared__ R4<R> wlm_tab[Trav::kLdsMats];
       for (uint32_t j = threadIdx.x; j < p.sc.n_mats; j += kBlock) {
         const Material<R>& m = p.sc.mats[j];
-        wlm_tab[j] = R4<R>{m.tx.c0[0], m.tx.c0[1], m.tx.c0[2], m.kind == M_DIFFUSE_LIGHT ? R(1) : R(0)};
+        wlm_tab[j] = R4<R>{m.tx.c0[0], m.tx.c0[1], m.tx.c0[2],
+                           m.kind == M_DIFFUSE_LIGHT ? R(1) : (m.kind == M_ISOTROPIC ? R(2) : R(0))};
       }
       __syncthreads();
       wlm = wlm_tab;
@@ -1404,14 +1423,17 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
         }
 #ifdef RT_SECTION_CLOCKS
         const uint64_t c1 = clock64();
-        const bool more = shade<R, CAMX, Trav::kFlat>(q, s, t, e, inst, nm);
+        const bool more = shade<R, CAMX, Trav::kFlat, true, Trav::kLinLL, Trav::kLinLL, false, Trav::kLinLL>(
+            q, s, t, e, inst, nm, nullptr, wlm);
         if (__lane_id() == (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1) {
           atomicAdd(wide_stats_lds() + 6, (unsigned long long)(c1 - c0));
           atomicAdd(wide_stats_lds() + 7, (unsigned long long)(clock64() - c1));
         }
         if (!more) break;
 #else
-        if (!shade<R, CAMX, Trav::kFlat>(q, s, t, e, inst, nm)) break;
+        if (!shade<R, CAMX, Trav::kFlat, true, Trav::kLinLL, Trav::kLinLL, false, Trav::kLinLL>(q, s, t, e, inst, nm,
+                                                                                            nullptr, wlm))
+          break;
 #endif
       }
     }
@@ -1948,8 +1970,15 @@ bool no_light_scene(const SceneHeader& h) {
   return (h.mat_kinds & ~ok_m) == 0 && (h.tex_kinds & ~((1u << T_SOLID) | (1u << T_CHECKER))) == 0 &&
          h.light_kind == L_NONE;
 }
+// lambertian, isotropic and diffuse_light materials with solid textures and an axis-aligned quad light (C5)
+bool lamb_iso_light_scene(const SceneHeader& h) {
+  const uint32_t ok_m = (1u << M_LAMBERTIAN) | (1u << M_DIFFUSE_LIGHT) | (1u << M_ISOTROPIC);
+  return (h.mat_kinds & ~ok_m) == 0 && (h.tex_kinds & ~(1u << T_SOLID)) == 0 && h.light_kind == L_QUAD &&
+         h.light_aligned != 0;
+}
 template <class R>
-void launch_step(const Params<R>& p, KernelFamily fam, bool ll, bool nl, int stack, uint32_t grid, hipStream_t st) {
+void launch_step(const Params<R>& p, KernelFamily fam, bool ll, bool nl, bool lli, int stack, uint32_t grid,
+                 hipStream_t st) {
   switch (fam) {
     case KF_FLAT:
       if constexpr (family_built(KF_FLAT)) {
@@ -1967,7 +1996,12 @@ void launch_step(const Params<R>& p, KernelFamily fam, bool ll, bool nl, int sta
       if constexpr (family_built(KF_LIN_QUAD)) launch_k<R, LinearTrav<R, false, false, false>>(p, grid, st);
       return;
     case KF_LIN_VOL:
-      if constexpr (family_built(KF_LIN_VOL)) launch_k<R, LinearTrav<R, false, false, true>>(p, grid, st);
+      if constexpr (family_built(KF_LIN_VOL)) {
+        if (RT_LIN_LLI && lli && p.sc.n_mats <= 16)  // lambertian + isotropic + light (C5)
+          launch_k<R, LinearTrav<R, false, false, true, true>>(p, grid, st);
+        else
+          launch_k<R, LinearTrav<R, false, false, true>>(p, grid, st);
+      }
       return;
     case KF_LIN_SPH:
       if constexpr (family_built(KF_LIN_SPH)) launch_k<R, LinearTrav<R, true, false, false>>(p, grid, st);
@@ -2092,7 +2126,7 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     const KernelFamily fam = kernel_family(hdr, cam->mode, persist, prm->traversal == RT_TRAV_ORDERED);
     if (!family_built(fam))
       return set_err(c, RT_ERR_UNSUPPORTED, std::string("this build (RT_DEV_ONLY) has no ") + family_name(fam) + " kernels");
-    const bool ll = lamb_light_scene(hdr), nl = no_light_scene(hdr);
+    const bool ll = lamb_light_scene(hdr), nl = no_light_scene(hdr), lli = lamb_iso_light_scene(hdr);
     uint32_t P = prm->pool_slots > 0 ? (uint32_t)prm->pool_slots
                  : persist       ? kAutoPersistLanes
                                  : (f64 ? kAutoPool64 : kAutoPool32);
@@ -2200,11 +2234,11 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
           hipEvent_t e0 = take_event(c, ev0 + ev), e1 = take_event(c, ev0 + ev + 1);
           if (!e0 || !e1) return set_err(c, RT_ERR_HIP, "hipEventCreate failed");
           RT_HIP(c, hipEventRecord(e0, st));
-          launch_step<R>(p, fam, ll, nl, cs.stack_need, grid, st);
+          launch_step<R>(p, fam, ll, nl, lli, cs.stack_need, grid, st);
           RT_HIP(c, hipEventRecord(e1, st));
           ev += 2;
         } else {
-          launch_step<R>(p, fam, ll, nl, cs.stack_need, grid, st);
+          launch_step<R>(p, fam, ll, nl, lli, cs.stack_need, grid, st);
         }
         RT_HIP(c, hipGetLastError());
         c->last.grid_lanes = t_grid_lanes;
@@ -2234,11 +2268,11 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
               hipEvent_t e0 = take_event(c, ev0 + ev), e1 = take_event(c, ev0 + ev + 1);
               if (!e0 || !e1) return set_err(c, RT_ERR_HIP, "hipEventCreate failed");
               RT_HIP(c, hipEventRecord(e0, st));
-              launch_step<R>(p, fam, ll, nl, cs.stack_need, grid, st);
+              launch_step<R>(p, fam, ll, nl, lli, cs.stack_need, grid, st);
               RT_HIP(c, hipEventRecord(e1, st));
               ev += 2;
             } else {
-              launch_step<R>(p, fam, ll, nl, cs.stack_need, grid, st);
+              launch_step<R>(p, fam, ll, nl, lli, cs.stack_need, grid, st);
             }
             launches++;
             iters++;
