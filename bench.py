@@ -284,6 +284,50 @@ def parity_tiles(fb, W, tiles, ref, rel_tol=None):
     return out
 
 
+def lit_parity(ctx, width, aspect, spp, depth, seed, threads, precisions, budget_s=20.0, ts=16):
+    """C4's kernel and tree on lit pixels (round-4 verdict): `sponza_lit` is the C4 stand-in -- the same
+    262,267 triangles, the same tree, the reference's light -- plus one unsampled diffuse_light quad under the
+    stand-in's grid over the camera (scenes/config_scenes.cpp). Seeded random 16x16 tiles of the full
+    1920x1080 frame at C4's own spp and depth, the oracle's first tiles that fit `budget_s`, against the GPU's
+    same tiles in each precision. Runs after the timed region (it uploads another scene)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    cs = plugin.ConfigScene("sponza_lit", width, aspect)
+    cam = cs.cam
+    W, H = cam.image_width, cam.image_height
+    tiles = [(x, y, min(ts, W - x), min(ts, H - y)) for y in range(0, H, ts) for x in range(0, W, ts)]
+    order = [tiles[i] for i in np.random.default_rng(seed + 11).permutation(len(tiles))]
+    osc = oracle.from_desc(cs.desc)
+    t0 = time.perf_counter()
+    done, sample = [], []
+    while order and time.perf_counter() - t0 < budget_s:
+        batch, order = order[:4], order[4:]
+        img, _ = oracle.render(osc, cam, spp, depth, seed=seed, threads=threads, tiles=batch)
+        done.append(img)
+        sample += batch
+    ref = np.concatenate(done)
+    st, info, _ = abi.scene_check(cs.desc)
+    # a tree takes the LDS-resident kernel only when all of it fits a block's 40 KiB (rt_kernels.hip
+    # wide_lds_bytes; a node is >= 48 B there): C4's 59,888 nodes take the HBM kernel C4 times
+    out = {"scene": "sponza_lit: the C4 stand-in + a second (unsampled) light under its grid over the camera",
+           "triangles": info.triangles, "wide_nodes": info.wide_nodes, "tree_in_hbm": info.wide_nodes * 48 > 40 << 10,
+           "oracle_s": round(time.perf_counter() - t0, 1)}
+    ctx.upload(cs.desc)
+    for prec in precisions:
+        got = ctx.render(cam, spp, depth, seed=seed, precision=prec, tiles=sample).astype(np.float64)
+        d = got - ref
+        rmse = np.sqrt((d ** 2).reshape(-1, 3).mean(0))
+        r = {"rmse": [float(f"{x:.3g}") for x in rmse], "max_abs": float(f"{np.abs(d).max():.3g}"),
+             "tiles": len(sample), "pixels": int(d.shape[0]), "mean_radiance": float(f"{ref.mean():.4g}"),
+             "lit_pixels": int((ref.max(-1) > 1e-3).sum()), "tolerance": 1e-4,
+             "pass": bool((rmse < 1e-4).all() and np.isfinite(got).all())}
+        if prec == abi.RT_PREC_F64:
+            bad = (np.abs(d) > 1e-9 * np.maximum(1.0, np.abs(ref))).any(-1)
+            r.update({"rel_tol": 1e-9, "pixels_over_rel_tol": int(bad.sum())})
+        out["fp64" if prec == abi.RT_PREC_F64 else "fp32"] = r
+    return out
+
+
 class Hip:
     """The few HIP runtime calls bench.py's copy stream needs, through ctypes (libamdhip64 is loaded by torch)."""
 
@@ -445,6 +489,7 @@ def main():
     ap.add_argument("--kernel-timing", default="on", choices=["on", "off"],
                     help="HIP events around every extend/shade launch of the timed steps (roofline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-lit-parity", action="store_true", help="C4: skip the lit stand-in parity leg")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: the CPUs this process may use, capped by the "
                                                                    "box's share (cgroup quota / OMP_NUM_THREADS)")
     ap.add_argument("--cpu-msamples", type=float, default=600.0,
@@ -604,6 +649,10 @@ def main():
                 alt_line["parity"] = parity_tiles(fba, W, ptiles, ref_px, rel_tol=1e-9 if alt_name == "f64" else None)
                 alt_line["speedup_vs_cpu_baseline"] = round(va / cpu["value"], 1)
                 alt_line["speedup_per_segment"] = round(va * sa / (cpu["value"] * cpu["segments_per_sample"]), 1)
+        lit = None
+        if cpu and scene_name == "sponza" and not args.no_lit_parity:
+            lit = lit_parity(ctx, width, aspect, spp, depth, args.seed, threads,
+                             [prec] + ([alt_prec] if alt_run is not None else []))
         line = {
             "metric": "Msamples/sec (pixels*spp) Cornell Box 800x800@1024spp; 1/2/4/8-GPU scaling"
             if args.config == "c2" else f"Msamples/sec (pixels*spp) {scene_name} {W}x{H}@{spp}spp",
@@ -626,6 +675,8 @@ def main():
             "parity": parity,
             alt_name: alt_line,
         }
+        if lit is not None:
+            line["lit_parity"] = lit
         if cpu:
             line["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
             # per unit of work: the GPU stops zero-throughput paths, the oracle does not, so

@@ -242,7 +242,11 @@ std::vector<std::array<vec3, 3>> gltf_triangles(std::vector<OutputPrimitives>& p
 }
 
 // main.cc:439-498. The asset path is $RT_SPONZA_GLTF, else the reference's relative path.
-void sponza(int width, double aspect, config_scene* s) {
+// `lit` (sponza_lit, not a reference scene): the same triangles and light plus a second, unsampled
+// diffuse_light quad facing down just under the stand-in's grid at y = 359 over the camera, so that C4's
+// tree and kernel are compared on lit pixels (the stand-in's grids close the atrium under the
+// reference's light at y = 1200, and its own frame is nearly black).
+void sponza(int width, double aspect, config_scene* s, bool lit = false) {
   const char* env = std::getenv("RT_SPONZA_GLTF");
   gltf::GltfLoader model(env && *env ? env : "./assets/Sponza/glTF/Sponza.gltf");
   auto& prims = model.getOutputPrimitives();
@@ -253,6 +257,9 @@ void sponza(int width, double aspect, config_scene* s) {
   auto light = std::make_shared<diffuse_light>(color(10));
   auto quad_light = std::make_shared<quad>(point3(0, 1200, 0), vec3(500, 0, 0), vec3(0, 0, 500), light);
   world.push_back(quad_light);
+  if (lit)
+    world.push_back(std::make_shared<quad>(point3(-400, 350, -250), vec3(800, 0, 0), vec3(0, 0, 500),
+                                           std::make_shared<diffuse_light>(color(1))));
   s->world = std::make_shared<bvh_node>(world);
   s->light = quad_light;
   s->cam.initialize_perspective(W(width, 200), A(aspect, 1.0), point3(500, 320, 90), point3(0, 280, 0), 1, 45.0, 30,
@@ -295,6 +302,8 @@ bool build_config_scene(const std::string& name, int width, double aspect, confi
     three_material_ball_with_defocus_blur(width, aspect, out);
   else if (name == "sponza")
     sponza(width, aspect, out);
+  else if (name == "sponza_lit")
+    sponza(width, aspect, out, true);
   else if (name == "glass_fox")
     glass_fox(width, aspect, out);
   else if (name == "skybox_and_fisheye")
