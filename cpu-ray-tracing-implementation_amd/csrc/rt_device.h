@@ -405,6 +405,8 @@ struct DevScene {
   uint32_t wide_big;  // primitives at the head of the word stream, tested before the tree
   uint32_t wide_top;  // nodes [0, wide_top): the tree's first levels (HBM trees: read from an LDS copy)
   const WNodeH* wnodesh;  // the fp16 form of the tree (rt_scene.h WNodeH; 0: none)
+  const double4w* wprims64;  // fp32 scenes with wide-tree quads: the fp64 words (RT_QUAD_REFINE; 0: none)
+  const Quad<double>* quads64;  // fp32 scenes: the fp64 quads (RT_QUAD_REFINE; 0: none)
   // a tree in HBM keeps at most wide_lds_stack<R>() stack entries per lane in LDS; deeper entries go to
   // wide_spill[(depth - wide_lds_stack<R>()) * spill_lanes + lane]
   uint32_t* wide_spill;
@@ -514,9 +516,51 @@ __device__ __forceinline__ bool quad_test(V<R> n, R D, V<R> q, V<R> qa, V<R> qb,
   t = th;
   return true;
 }
+// The fp32 test of a wide-tree quad, whose edges fp32 decides to ~1e-7 of the quad's size plus the rounding of
+// the hit point to its world-space magnitude (1.5e-5 at 400: a camera ray over the f3 scene's light edge at
+// x = 423 lands on 423.0f and hits, where fp64 misses -- 21 such samples of emission 7 were f3's whole fp32
+// RMSE of 1.1e-4, round 5). A hit whose alpha or beta lies within 2^-12 of 0 or 1 is re-decided in fp64 on
+// the same (fp32) ray with the quad's fp64 record (same word index in the fp64 words, rec64): the edge then
+// moves with the ray's own rounding only. Rare (a few 1e-4 of the tests that pass the distance test).
+#ifndef RT_QUAD_REFINE
+#define RT_QUAD_REFINE 1
+#endif
+template <class REF>
+__device__ __forceinline__ bool quad_test_near(V<float> n, float D, V<float> q, V<float> qa, V<float> qb, V<float> o,
+                                               V<float> d, float tmin, float tmax, float& t, bool have64, REF ref64) {
+  const float th = fdiv(D - dot(n, o), dot(n, d));
+  if (!(tmin <= th && th <= tmax)) return false;  // interval::is_contains, NaN fails
+  const V<float> p = (o + th * d) - q;
+  const float a = dot(p, qa), b = dot(p, qb);
+  const float m = fminf(fminf(fabsf(a), fabsf(a - 1.0f)), fminf(fabsf(b), fabsf(b - 1.0f)));
+  if (have64 && m < 0x1p-12f) {
+    double t64;
+    if (!ref64(mkv((double)o.x, (double)o.y, (double)o.z), mkv((double)d.x, (double)d.y, (double)d.z), (double)tmin,
+               (double)tmax, t64))
+      return false;
+    t = th;
+    return true;
+  }
+  if (!(0.0f <= a && a <= 1.0f && 0.0f <= b && b <= 1.0f)) return false;  // quad.h:58-64
+  t = th;
+  return true;
+}
 template <class R>
 __device__ __forceinline__ bool quad_t(const Quad<R>& q, V<R> o, V<R> d, R tmin, R tmax, R& t) {
   return quad_test(ld3(q.n), q.D, ld3(q.q), ld3(q.a), ld3(q.b), o, d, tmin, tmax, t);
+}
+// quad i of the scene (binary BVH traversal); fp32 with the fp64 re-decision near an edge
+template <class R>
+__device__ __forceinline__ bool quad_t_near(const DevScene<R>& sc, uint32_t i, V<R> o, V<R> d, R tmin, R tmax, R& t) {
+  const Quad<R>& q = sc.quads[i];
+  if constexpr (sizeof(R) == 4 && RT_QUAD_REFINE) {
+    const Quad<double>* q64 = sc.quads64;
+    return quad_test_near(ld3(q.n), q.D, ld3(q.q), ld3(q.a), ld3(q.b), o, d, tmin, tmax, t, q64 != nullptr,
+                          [&](V<double> od, V<double> dd, double t0, double t1, double& t64) {
+                            return quad_t(q64[i], od, dd, t0, t1, t64);
+                          });
+  }
+  return quad_t(q, o, d, tmin, tmax, t);
 }
 
 // triangle::hit / moller_trumbore (triangle.h:8-40).
@@ -931,7 +975,7 @@ __device__ void trace(const DevScene<R>& sc, const Node<R>* nodes, V<R> wo, V<R>
     bool h;
     if (ty == E_QUAD) {
       if (self) return;
-      h = quad_t(sc.quads[i], o, d, tmin, tmax, th);
+      h = quad_t_near(sc, i, o, d, tmin, tmax, th);
     } else if (ty == E_SPHERE) {
       h = sphere_t(sc.spheres[i], o, d, time, tmin, tmax, self, th);
     } else {
@@ -1386,9 +1430,21 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
         hit = e != excl_e && tri_test(mkv(h.x, h.y, h.z), mkv(a.x, a.y, a.z), mkv(b.x, b.y, b.z), ro, rd, tmin, tmax, th);
       } else if (QUAD) {
         const WW nD = PF ? a1 : pw(w + 1), qa = PF ? a2 : pw(w + 2), qb = pw(w + 3);
+        if constexpr (sizeof(R) == 4 && RT_QUAD_REFINE) {
+          const double4w* r64 = sc.wprims64 + w;
+          hit = e != excl_e &&
+                quad_test_near(mkv(nD.x, nD.y, nD.z), nD.w, mkv(h.x, h.y, h.z), mkv(qa.x, qa.y, qa.z),
+                               mkv(qb.x, qb.y, qb.z), ro, rd, tmin, tmax, th, sc.wprims64 != nullptr,
+                               [&](V<double> od, V<double> dd, double t0, double t1, double& t64) {
+                                 const double4w g0 = r64[0], g1 = r64[1], g2 = r64[2], g3 = r64[3];
+                                 return quad_test(mkv(g1.x, g1.y, g1.z), g1.w, mkv(g0.x, g0.y, g0.z),
+                                                  mkv(g2.x, g2.y, g2.z), mkv(g3.x, g3.y, g3.z), od, dd, t0, t1, t64);
+                               });
+        } else {
+          hit = e != excl_e && quad_test(mkv(nD.x, nD.y, nD.z), nD.w, mkv(h.x, h.y, h.z), mkv(qa.x, qa.y, qa.z),
+                                         mkv(qb.x, qb.y, qb.z), ro, rd, tmin, tmax, th);
+        }
         w += 4;
-        hit = e != excl_e && quad_test(mkv(nD.x, nD.y, nD.z), nD.w, mkv(h.x, h.y, h.z), mkv(qa.x, qa.y, qa.z),
-                                       mkv(qb.x, qb.y, qb.z), ro, rd, tmin, tmax, th);
       }
       if (hit) {
         tmax = th;

@@ -1401,6 +1401,11 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
   h.off_wnodes = append(out->blob32, wn);
   h.has_wnodesh = 0;  // only fp64 rays read the fp16 form (RT_WIDE_HALF_F64): it stays out of the fp32 blob
   h.off_wprims = append(out->blob32, words);
+  h.has_wprims64 = 0;
+  if (kinds & WK_QUAD) {  // the fp32 quad test re-decides hits near an edge in fp64 (rt_device.h trace_wide)
+    h.off_wprims64 = append(out->blob32, words64);
+    h.has_wprims64 = 1;
+  }
   out->blob32.resize((out->blob32.size() + 255) & ~size_t(255));
   h.bytes = out->blob32.size();
   h.n_wnodes = (uint32_t)wn.size();
@@ -1570,6 +1575,12 @@ bool Compiler::run(CompiledScene* out, std::string* err) {
       pack(out->blob64, quads_, spheres_, tris_, insts_, vols_, nodes_, refs_, mats_, texs_, light_, linear, texdata_, images_);
   out->hdr = pack(out->blob32, map32(quads_), map32(spheres_), map32(tris_), map32(insts_), map32(vols_),
                   map32(nodes_), refs_, map32(mats_), map32(texs_), to32(light_), map32(linear), texdata_, images_);
+  if (!quads_.empty()) {  // the fp32 quad test re-decides hits near an edge in fp64 (rt_device.h quad_t)
+    out->hdr.off_quads64 = append(out->blob32, quads_);
+    out->hdr.has_quads64 = 1;
+    out->blob32.resize((out->blob32.size() + 255) & ~size_t(255));
+    out->hdr.bytes = out->blob32.size();
+  }
   if (has_flat) {
     std::vector<FlatQuadT<float>> fq32;
     std::vector<FlatBoxT<float>> fb32;
