@@ -86,8 +86,8 @@ constexpr int kBlock = 256;
 #ifndef RT_LIN_LLI  // the volume program for lambertian + isotropic + light scenes (shade LL, LLI): C5 fp32
 #define RT_LIN_LLI 1  // 1,189 -> 1,124 ms/frame, fp64 2,358 -> 2,262 (r05y)
 #endif
-#ifndef RT_LINEAR_VOL_WAVES_LLI  // its fp32 form at 7 waves (79 VGPRs at 6): 1,124 -> 1,097 ms/frame (r05y)
-#define RT_LINEAR_VOL_WAVES_LLI 7
+#ifndef RT_LINEAR_VOL_WAVES_LLI  // its fp32 form at 7 waves (79 VGPRs at 6): 1,124 -> 1,097 ms/frame (r05y); 8 (64
+#define RT_LINEAR_VOL_WAVES_LLI 8  // VGPRs + 60 B spilled): 1,098 -> 1,080 (r05v2). (C3 fp64 NL at 6 waves: 65.2 -> 69.5)
 #endif
 #ifndef RT_LINEAR_VOL_WAVES_F64  // the fp64 volume program (round 4, cold state in LDS): 3 waves 2,672 ms/frame, 4: 2,400
 #define RT_LINEAR_VOL_WAVES_F64 4
@@ -961,7 +961,8 @@ struct LinearTrav {
 #define RT_FLAT_LDS 1
 #endif
 #ifndef RT_FLAT_WAVES_F64_LL  // the same for the lambertian + light kernel
-#define RT_FLAT_WAVES_F64_LL 6  // C2 fp64: 5 waves 28.90 ms/frame, 6: 28.08 (r05c; the general kernel at 5: 31.28)
+#define RT_FLAT_WAVES_F64_LL 7  // C2 fp64: 5 waves 28.90 ms/frame, 6: 28.08 (r05c; the general kernel at 5: 31.28);
+                                // 7 (72 VGPRs + 32 B spilled, from 80): 27.94 -> 27.79 (r05w7); 8 does not fit
 #endif
 #ifndef RT_FLAT_LL  // flat program: a kernel for lambertian + light scenes (shade LL)
 #define RT_FLAT_LL 1
