@@ -127,6 +127,13 @@ def load():
         path = lib_path()
         if not os.path.exists(path):
             raise RuntimeError(f"{path} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        # One HIP runtime per process: librt_hip needs libamdhip64.so.7, and so does PyTorch, which bundles its
+        # own. Loaded first, librt_hip would bring in /opt/rocm's, and a later `import torch` would bind to that
+        # one and find no GPU ("No HIP GPUs are available"). PyTorch first, librt_hip then binds to its runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         lib = ctypes.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name)
