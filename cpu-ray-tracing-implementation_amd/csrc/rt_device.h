@@ -405,7 +405,6 @@ struct DevScene {
   uint32_t wide_big;  // primitives at the head of the word stream, tested before the tree
   uint32_t wide_top;  // nodes [0, wide_top): the tree's first levels (HBM trees: read from an LDS copy)
   const WNodeH* wnodesh;  // the fp16 form of the tree (rt_scene.h WNodeH; 0: none)
-  const double4w* wprims64;  // fp32 scenes with wide-tree quads: the fp64 words (RT_QUAD_REFINE; 0: none)
   const Quad<double>* quads64;  // fp32 scenes: the fp64 quads (RT_QUAD_REFINE; 0: none)
   // a tree in HBM keeps at most wide_lds_stack<R>() stack entries per lane in LDS; deeper entries go to
   // wide_spill[(depth - wide_lds_stack<R>()) * spill_lanes + lane]
@@ -520,8 +519,8 @@ __device__ __forceinline__ bool quad_test(V<R> n, R D, V<R> q, V<R> qa, V<R> qb,
 // the hit point to its world-space magnitude (1.5e-5 at 400: a camera ray over the f3 scene's light edge at
 // x = 423 lands on 423.0f and hits, where fp64 misses -- 21 such samples of emission 7 were f3's whole fp32
 // RMSE of 1.1e-4, round 5). A hit whose alpha or beta lies within 2^-12 of 0 or 1 is re-decided in fp64 on
-// the same (fp32) ray with the quad's fp64 record (same word index in the fp64 words, rec64): the edge then
-// moves with the ray's own rounding only. Rare (a few 1e-4 of the tests that pass the distance test).
+// the same (fp32) ray with the quad's fp64 record (ref64; the binary-BVH traversal, quad_t_near): the edge
+// then moves with the ray's own rounding only. Rare (a few 1e-4 of the tests that pass the distance test).
 #ifndef RT_QUAD_REFINE
 #define RT_QUAD_REFINE 1
 #endif
@@ -1430,20 +1429,10 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
         hit = e != excl_e && tri_test(mkv(h.x, h.y, h.z), mkv(a.x, a.y, a.z), mkv(b.x, b.y, b.z), ro, rd, tmin, tmax, th);
       } else if (QUAD) {
         const WW nD = PF ? a1 : pw(w + 1), qa = PF ? a2 : pw(w + 2), qb = pw(w + 3);
-        if constexpr (sizeof(R) == 4 && RT_QUAD_REFINE) {
-          const double4w* r64 = sc.wprims64 + w;
-          hit = e != excl_e &&
-                quad_test_near(mkv(nD.x, nD.y, nD.z), nD.w, mkv(h.x, h.y, h.z), mkv(qa.x, qa.y, qa.z),
-                               mkv(qb.x, qb.y, qb.z), ro, rd, tmin, tmax, th, sc.wprims64 != nullptr,
-                               [&](V<double> od, V<double> dd, double t0, double t1, double& t64) {
-                                 const double4w g0 = r64[0], g1 = r64[1], g2 = r64[2], g3 = r64[3];
-                                 return quad_test(mkv(g1.x, g1.y, g1.z), g1.w, mkv(g0.x, g0.y, g0.z),
-                                                  mkv(g2.x, g2.y, g2.z), mkv(g3.x, g3.y, g3.z), od, dd, t0, t1, t64);
-                               });
-        } else {
-          hit = e != excl_e && quad_test(mkv(nD.x, nD.y, nD.z), nD.w, mkv(h.x, h.y, h.z), mkv(qa.x, qa.y, qa.z),
-                                         mkv(qb.x, qb.y, qb.z), ro, rd, tmin, tmax, th);
-        }
+        // (no fp64 re-decision near edges here, unlike quad_t_near: its registers spilled the C4 fp32 kernel,
+        // 8 -> 104 B per lane, 264 -> 288 ms/frame, r05fin; the wide kernels with quads are the triangle ones)
+        hit = e != excl_e && quad_test(mkv(nD.x, nD.y, nD.z), nD.w, mkv(h.x, h.y, h.z), mkv(qa.x, qa.y, qa.z),
+                                       mkv(qb.x, qb.y, qb.z), ro, rd, tmin, tmax, th);
         w += 4;
       }
       if (hit) {

@@ -1813,7 +1813,6 @@ DevScene<R> dev_scene(const SceneHeader& h, void* base) {
   s.wide_big = h.wide_big;
   s.wide_top = h.wide_top;
   s.wnodesh = h.has_wnodesh ? (const WNodeH*)at(h.off_wnodesh) : nullptr;
-  s.wprims64 = h.has_wprims64 ? (const double4w*)at(h.off_wprims64) : nullptr;
   s.quads64 = h.has_quads64 ? (const Quad<double>*)at(h.off_quads64) : nullptr;
   return s;
 }

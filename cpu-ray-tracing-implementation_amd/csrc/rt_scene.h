@@ -312,10 +312,6 @@ struct SceneHeader {
   uint32_t wide_big;     // primitives at the head of the word stream tested before the tree (huge boxes)
   uint32_t has_wnodesh;  // the WNodeH form of the same tree is present (n_wnodes nodes from off_wnodesh)
   uint64_t off_wnodesh;
-  // fp32 blob of a wide tree with quads: the fp64 primitive words too (same word indices), read by the fp32
-  // quad test for hits near an edge (trace_wide, RT_QUAD_REFINE); 0: none
-  uint32_t has_wprims64;
-  uint64_t off_wprims64;
   // fp32 blob: the fp64 Quad records too (same indices), for the same re-decision in quad_t; 0: none
   uint32_t has_quads64;
   uint64_t off_quads64;

@@ -1401,11 +1401,6 @@ bool Compiler::wide_bvh(const std::vector<Item>& all, CompiledScene* out) {
   h.off_wnodes = append(out->blob32, wn);
   h.has_wnodesh = 0;  // only fp64 rays read the fp16 form (RT_WIDE_HALF_F64): it stays out of the fp32 blob
   h.off_wprims = append(out->blob32, words);
-  h.has_wprims64 = 0;
-  if (kinds & WK_QUAD) {  // the fp32 quad test re-decides hits near an edge in fp64 (rt_device.h trace_wide)
-    h.off_wprims64 = append(out->blob32, words64);
-    h.has_wprims64 = 1;
-  }
   out->blob32.resize((out->blob32.size() + 255) & ~size_t(255));
   h.bytes = out->blob32.size();
   h.n_wnodes = (uint32_t)wn.size();
