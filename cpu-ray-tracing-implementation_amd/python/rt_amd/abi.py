@@ -112,6 +112,24 @@ SIGNATURES = {
     "rt_multi_comm_inits": (c_uint64, []),
 }
 
+
+class TileList:
+    """A tile list as the ctypes array rt_render_tiles takes, built once: a caller that renders the same
+    tiles every frame (rt_amd.distributed.FrameSharding) passes this instead of a list, whose conversion
+    (one rt_tile per 16x16 tile: C1's 625, C2's 2,500) costs ~1 us of Python per tile and call."""
+
+    def __init__(self, tiles):
+        self.tiles = [tuple(t) for t in tiles]
+        self.n = len(self.tiles)
+        self.arr = (rt_tile * max(1, self.n))(*[rt_tile(*t) for t in self.tiles])
+
+    def __len__(self):
+        return self.n
+
+    def __iter__(self):
+        return iter(self.tiles)
+
+
 _lib = None
 
 
@@ -130,6 +148,7 @@ def load():
         # One HIP runtime per process: librt_hip needs libamdhip64.so.7, and so does PyTorch, which bundles its
         # own. Loaded first, librt_hip would bring in /opt/rocm's, and a later `import torch` would bind to that
         # one and find no GPU ("No HIP GPUs are available"). PyTorch first, librt_hip then binds to its runtime.
+        # (plugin.load goes through here too: librt_scenes links librt_hip.)
         try:
             import torch  # noqa: F401
         except ImportError:

@@ -11,6 +11,7 @@ random numbers are keyed by (seed, global pixel, sample) and the item layout by 
 import torch
 import torch.distributed as dist
 
+from .abi import TileList
 from .tiling import pixel_index, plan
 
 
@@ -21,6 +22,7 @@ class FrameSharding:
         self.W, self.H, self.world, self.rank, self.device, self.group = width, height, world, rank, device, group
         self.tiles, self.counts, self.maxpix = plan(width, height, world)
         self.my_tiles = self.tiles[rank]
+        self._my_tiles_c = TileList(self.my_tiles)  # the ctypes form, built once (render_tiles)
         self.backend = dist.get_backend(group) if world > 1 else None
         self.scatter_idx = None
         self._recv = {}  # rank 0's gather buffers, per (dtype, device), reused frame to frame
@@ -40,9 +42,9 @@ class FrameSharding:
         another stream is joined to it by an event first."""
         if stream is None:
             handle = torch.cuda.current_stream(self.device).cuda_stream
-            ctx.render_tiles(cam, params, self.my_tiles, out.data_ptr(), 1, handle)
+            ctx.render_tiles(cam, params, self._my_tiles_c, out.data_ptr(), 1, handle)
         elif isinstance(stream, torch.cuda.Stream):
-            ctx.render_tiles(cam, params, self.my_tiles, out.data_ptr(), 1, stream.cuda_stream)
+            ctx.render_tiles(cam, params, self._my_tiles_c, out.data_ptr(), 1, stream.cuda_stream)
             cur = torch.cuda.current_stream(self.device)
             if stream != cur:
                 ev = torch.cuda.Event()
@@ -52,7 +54,7 @@ class FrameSharding:
             if torch.cuda.is_available() and stream not in (0, torch.cuda.current_stream(self.device).cuda_stream):
                 raise ValueError("pass a torch.cuda.Stream: a raw handle of another stream cannot be ordered "
                                  "before the gather")
-            ctx.render_tiles(cam, params, self.my_tiles, out.data_ptr(), 1, stream)
+            ctx.render_tiles(cam, params, self._my_tiles_c, out.data_ptr(), 1, stream)
         if self.world == 1:
             parts = [out]
         elif self.backend == "gloo":  # host-memory gather (the device buffer is copied behind the render)

@@ -15,6 +15,7 @@ def load():
         path = os.path.join(abi.BUILD_DIR, "librt_scenes.so")
         if not os.path.exists(path):
             raise RuntimeError(f"{path} is missing: run `make`")
+        abi.load()  # librt_scenes links librt_hip: loaded the way abi.load does (PyTorch's HIP runtime first)
         L = ctypes.CDLL(path)
         P = ctypes.POINTER
         L.rtsc_build.restype = ctypes.c_void_p

@@ -53,7 +53,8 @@ class Context:
                                     traversal=traversal)
 
     def render_tiles(self, cam, params, tiles, out_ptr, out_is_device, stream=None):
-        arr = (abi.rt_tile * max(1, len(tiles)))(*[abi.rt_tile(*t) for t in tiles])
+        """`tiles`: a list of (x, y, w, h), or an abi.TileList built once for tiles rendered every frame."""
+        arr = tiles.arr if isinstance(tiles, abi.TileList) else abi.TileList(tiles).arr
         self._check(self.lib.rt_render_tiles(self.h, ctypes.byref(cam), ctypes.byref(params), arr, len(tiles),
                                              ctypes.c_void_p(out_ptr), int(out_is_device),
                                              ctypes.c_void_p(stream or 0)))
