@@ -46,6 +46,9 @@ using namespace rtd;
 namespace {
 
 constexpr int kBlock = 256;
+#ifndef RT_BG_BLACK_SKIP  // shade: no unit-sphere test for a miss against a solid black background
+#define RT_BG_BLACK_SKIP 1
+#endif
 #ifndef RT_CAM_BASE
 #define RT_CAM_BASE 1
 #endif
@@ -612,7 +615,12 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
     printf("[dev] bounce %d o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) miss\n", s.bounce, (double)o.x, (double)o.y,
            (double)o.z, (double)d.x, (double)d.y, (double)d.z);
 #endif
-    if (sc.background >= 0) {
+    // a solid black background (the Cornell configs' solid_color::black) adds thr * 0: the unit-sphere test
+    // that decides whether it is sampled (camera.h:183-187) is skipped (a wave-uniform test of the record)
+    const Texture<R>* bgt = sc.background >= 0 ? sc.texs + sc.background : nullptr;
+    const bool bg_black = RT_BG_BLACK_SKIP && bgt != nullptr && ld_here(&bgt->kind) == T_SOLID &&
+                          ld_here(&bgt->c0[0]) == R(0) && ld_here(&bgt->c0[1]) == R(0) && ld_here(&bgt->c0[2]) == R(0);
+    if (sc.background >= 0 && !bg_black) {
       R tb;
       if (sphere_roots<R>(o.x, o.y, o.z, d.x, d.y, d.z, o.x, o.y, o.z, R(1), R(0.001), Num<R>::inf(), false, tb)) {
         double bu = 0, bv = 0;
