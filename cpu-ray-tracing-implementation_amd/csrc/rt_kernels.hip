@@ -49,6 +49,9 @@ constexpr int kBlock = 256;
 #ifndef RT_BG_BLACK_SKIP  // shade: no unit-sphere test for a miss against a solid black background
 #define RT_BG_BLACK_SKIP 1
 #endif
+#ifndef RT_BG_SOLID_FAST  // shade: nor against another solid background when |d| < 500 (the test always hits)
+#define RT_BG_SOLID_FAST 1
+#endif
 #ifndef RT_CAM_BASE
 #define RT_CAM_BASE 1
 #endif
@@ -620,7 +623,15 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
     const Texture<R>* bgt = sc.background >= 0 ? sc.texs + sc.background : nullptr;
     const bool bg_black = RT_BG_BLACK_SKIP && bgt != nullptr && ld_here(&bgt->kind) == T_SOLID &&
                           ld_here(&bgt->c0[0]) == R(0) && ld_here(&bgt->c0[1]) == R(0) && ld_here(&bgt->c0[2]) == R(0);
-    if (sc.background >= 0 && !bg_black) {
+    // any other solid background: the unit sphere about the ray's origin has the root t = 1/|d|, inside
+    // [0.001, inf) for |d| < 1000, and a solid colour does not depend on where it is hit -- so for |d| < 500
+    // the colour is added without the test (RT_BG_SOLID_FAST; RTOW's sky, C3)
+    const bool bg_solid = RT_BG_SOLID_FAST && bgt != nullptr && !bg_black && ld_here(&bgt->kind) == T_SOLID &&
+                          dot(d, d) < R(250000);
+    if (bg_solid) {
+      add = s.thr * mkv(ld_here(&bgt->c0[0]), ld_here(&bgt->c0[1]), ld_here(&bgt->c0[2]));
+      has_add = true;
+    } else if (sc.background >= 0 && !bg_black) {
       R tb;
       if (sphere_roots<R>(o.x, o.y, o.z, d.x, d.y, d.z, o.x, o.y, o.z, R(1), R(0.001), Num<R>::inf(), false, tb)) {
         double bu = 0, bv = 0;
