@@ -329,12 +329,25 @@ def lit_parity(ctx, width, aspect, spp, depth, seed, threads, precisions, budget
 
 
 class Hip:
-    """The few HIP runtime calls bench.py's copy stream needs, through ctypes (libamdhip64 is loaded by torch)."""
+    """The few HIP runtime calls bench.py's copy stream needs, through ctypes, bound to the HIP runtime this
+    process already runs on (torch's bundled libamdhip64.so.7, which librt_hip shares): found in /proc/self/maps
+    and opened with RTLD_NOLOAD, so a second runtime (/opt/rocm's, by an unversioned name) is never loaded and
+    the stream and event handles torch hands over stay valid. Fails loudly if no runtime is loaded yet."""
 
     def __init__(self):
         import ctypes
         self.ct = ctypes
-        self.lib = ctypes.CDLL("libamdhip64.so")
+        path = None
+        with open("/proc/self/maps") as fh:
+            for line in fh:
+                f = line.split()
+                if len(f) >= 6 and os.path.basename(f[5]).startswith("libamdhip64.so"):
+                    path = f[5]
+                    break
+        if path is None:
+            raise RuntimeError("bench.py: no HIP runtime is loaded in this process (torch is imported and the "
+                               "GPU touched before Hip())")
+        self.lib = ctypes.CDLL(path, mode=os.RTLD_NOLOAD | os.RTLD_NOW)
         for name, args in (("hipEventCreateWithFlags", [ctypes.c_void_p, ctypes.c_uint]),
                            ("hipEventRecord", [ctypes.c_void_p, ctypes.c_void_p]),
                            ("hipStreamWaitEvent", [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]),

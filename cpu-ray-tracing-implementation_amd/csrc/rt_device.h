@@ -21,45 +21,29 @@ namespace rtd {
 #ifndef RT_WIDE_SPEC  // wide BVH in HBM: speculative while-while traversal (trace_wide)
 #define RT_WIDE_SPEC 1
 #endif
-#ifndef RT_WIDE_FMA  // fp64 rays over the wide BVH: octant-ordered planes, one fma per plane distance
-#define RT_WIDE_FMA 1
-#endif
-#ifndef RT_WIDE_OCT32  // fp32 rays over the wide BVH: octant-ordered planes, (p - o) * inv (C3 fp32 60.87 ->
-#define RT_WIDE_OCT32 1  // 57.22 ms/frame, C4 351.9 -> 341.6)
-#endif
-#ifndef RT_WIDE_HALF_F64  // fp64 rays over trees in HBM read the fp16 node form (rt_scene.h WNodeH): 5 loads per
-#define RT_WIDE_HALF_F64 1  // node visit instead of 7 (C4 fp64 504.0 -> 480.8 ms/frame; fp32 rays lose, see WNodeH)
-#endif
+// RT_WIDE_FMA (retired in round 6, always on): fp64 rays over the wide BVH: octant-ordered planes, one fma per plane
+// distance
+// RT_WIDE_OCT32 (retired in round 6, always on): fp32 rays over the wide BVH: octant-ordered planes, (p - o) * inv (C3
+// fp32 60.87 -> 57.22 ms/frame, C4 351.9 -> 341.6)
+// RT_WIDE_HALF_F64 (retired in round 6, always on): fp64 rays over trees in HBM read the fp16 node form (rt_scene.h
+// WNodeH): 5 loads per node visit instead of 7 (C4 fp64 504.0 -> 480.8 ms/frame; fp32 rays lose, see WNodeH)
 #ifndef RT_WIDE_FMA32  // fp32 rays over an LDS tree: one fma per plane distance, three per-ray constants and one
 #define RT_WIDE_FMA32 1  // bound (trace_wide; C3 fp32 49.63 -> 48.54 ms/frame; 2, per-axis constants: 49.01)
 #endif
-#ifndef RT_WIDE_OFS64  // fp64 rays keep 64-bit addresses into trees in HBM (C4 fp64: 32-bit offsets 573.5 ms/frame,
-#define RT_WIDE_OFS64 1  // 64-bit 545.1; fp32 the other way round, 340.7 -> 329.1)
-#endif
-#ifndef RT_WIDE_PREFETCH  // a triangle's words loaded with the record's first word (C4 358.9 -> 357.2 ms)
-#define RT_WIDE_PREFETCH 1
-#endif
+// RT_WIDE_OFS64 (retired in round 6, always on): fp64 rays keep 64-bit addresses into trees in HBM (C4 fp64: 32-bit
+// offsets 573.5 ms/frame, 64-bit 545.1; fp32 the other way round, 340.7 -> 329.1)
+// RT_WIDE_PREFETCH (retired in round 6, always on): a triangle's words loaded with the record's first word (C4 358.9 ->
+// 357.2 ms)
 // The extended (CAMX) kernels' heavy, rarely taken code -- fp64 OCML trigonometry (sphere_uv, the fisheye
 // camera), the noise textures -- as real calls (round 5): inlined, their temporaries sized the whole kernel
 // (~290 registers, 1 wave per SIMD); called, the loop keeps its own budget and the live state is saved
 // around the call only when it is taken.
-#ifndef RT_EXT_NOINLINE
-#define RT_EXT_NOINLINE 1
-#endif
-#if RT_EXT_NOINLINE
 #define RT_EXT_FN __device__ __attribute__((noinline))
-#else
-#define RT_EXT_FN __device__ __forceinline__
-#endif
 #ifndef RT_MIX_SELECT  // the light / material halves of the mixture pdf (pdf.h:52-56) as one select path: 1 in
 #define RT_MIX_SELECT 1  // the flat program (C2 fp64 28.33 -> 28.15 ms/frame, fp32 18.83 -> 18.49, r05e), 2 in every kernel
 #endif
-#ifndef RT_LIGHT_PDF_F64  // fp64 axis-aligned light pdf by one reciprocal (light_pdf_aligned, round 4)
-#define RT_LIGHT_PDF_F64 1
-#endif
-#ifndef RT_WIDE_OCTPACK
-#define RT_WIDE_OCTPACK 1
-#endif
+// RT_LIGHT_PDF_F64 (retired in round 6, always on): fp64 axis-aligned light pdf by one reciprocal (light_pdf_aligned,
+// round 4)
 
 // Math policy. fp64 (the parity path): libm where the reference calls it (log), and division,
 // reciprocal and square root refined from the hardware estimates to about an ulp (below).
@@ -370,6 +354,19 @@ struct WWord<double> {
 __device__ __forceinline__ uint32_t wentry(const float4& h) { return __float_as_uint(h.w); }
 __device__ __forceinline__ uint32_t wentry(const double4w& h) { return (uint32_t)__double_as_longlong(h.w); }
 
+// The camera as camera::render/generate_ray use it (camera.h:137-141, 244-290), in double.
+struct CamDev {
+  int32_t mode;  // rt_camera_mode
+  int32_t pad;
+  V<double> pos, du, dv;
+  V<double> dir00;   // perspective / fisheye: f dir - vw/2 right + vh/2 up + (du + dv)/2 (camera.h:246, 260)
+  V<double> pos00;   // orthonormal / lens: pos - vw/2 right + vh/2 up + (du + dv)/2 (camera.h:253, 278)
+  V<double> dir;     // dir_, unit
+  V<double> fdir;    // focus_dist_ * dir_ (camera.h:279)
+  V<double> disk_u, disk_v;  // defocus_disk_u/v (camera.h:129-131)
+  double focal;      // focal_length_ (camera.h:266)
+};
+
 template <class R>
 struct DevScene {
   const Quad<R>* quads;
@@ -406,20 +403,21 @@ struct DevScene {
   uint32_t wide_top;  // nodes [0, wide_top): the tree's first levels (HBM trees: read from an LDS copy)
   const WNodeH* wnodesh;  // the fp16 form of the tree (rt_scene.h WNodeH; 0: none)
   const Quad<double>* quads64;  // fp32 scenes: the fp64 quads (RT_QUAD_REFINE; 0: none)
+  // the render's camera when it is perspective (0: another model): near-edge quad hits of camera rays are re-decided
+  // on the fp64 camera ray (quad_edge64)
+  const CamDev* cam64;
   // a tree in HBM keeps at most wide_lds_stack<R>() stack entries per lane in LDS; deeper entries go to
   // wide_spill[(depth - wide_lds_stack<R>()) * spill_lanes + lane]
   uint32_t* wide_spill;
   uint32_t spill_lanes;
 };
-#ifndef RT_WIDE_TOP  // fp32 rays over trees in HBM: the tree's first levels read from LDS (trace_wide)
-#define RT_WIDE_TOP 1
-#endif
+// RT_WIDE_TOP (retired in round 6, always on): fp32 rays over trees in HBM: the tree's first levels read from LDS
+// (trace_wide)
 #ifndef RT_WIDE_TOP_N  // at most this many of them (the builder orders up to kWideTopMax breadth-first)
 #define RT_WIDE_TOP_N 55
 #endif
-#ifndef RT_WIDE_TOP_F64  // the same for fp64 rays, whose HBM trees are read in the fp16 form (WNodeH)
-#define RT_WIDE_TOP_F64 1
-#endif
+// RT_WIDE_TOP_F64 (retired in round 6, always on): the same for fp64 rays, whose HBM trees are read in the fp16 form
+// (WNodeH)
 #ifndef RT_WIDE_TOP_N_F64
 #define RT_WIDE_TOP_N_F64 85
 #endif
@@ -515,15 +513,36 @@ __device__ __forceinline__ bool quad_test(V<R> n, R D, V<R> q, V<R> qa, V<R> qb,
   t = th;
   return true;
 }
-// The fp32 test of a wide-tree quad, whose edges fp32 decides to ~1e-7 of the quad's size plus the rounding of
-// the hit point to its world-space magnitude (1.5e-5 at 400: a camera ray over the f3 scene's light edge at
-// x = 423 lands on 423.0f and hits, where fp64 misses -- 21 such samples of emission 7 were f3's whole fp32
-// RMSE of 1.1e-4, round 5). A hit whose alpha or beta lies within 2^-12 of 0 or 1 is re-decided in fp64 on
-// the same (fp32) ray with the quad's fp64 record (ref64; the binary-BVH traversal, quad_t_near): the edge
-// then moves with the ray's own rounding only. Rare (a few 1e-4 of the tests that pass the distance test).
+// Near-edge quad hits in fp32 (round 5, extended in round 6). fp32 decides a quad's edges to ~1e-7 of the quad's
+// size plus the rounding of the hit point to its world-space magnitude (1.5e-5 at 400: a camera ray over the f3
+// scene's light edge at x = 423 lands on 423.0f and hits, where fp64 misses -- 21 such samples of emission 7 were f3's
+// whole fp32 RMSE of 1.1e-4, round 5). A test whose alpha or beta lies within 2^-12 of 0 or 1 is re-decided in fp64
+// with the quad's fp64 record (DevScene::quads64) by quad_edge64, a call (RT_EXT_FN): rare (a few 1e-4 of the tests
+// that pass the distance test), so the kernels keep their register budget and pay for the call only when it is taken.
+// The fp64 ray is the path's own camera ray when the ray is one (bounce 0, world space, a perspective camera):
+// camera rays are built in fp64 (begin_sample) and rounded, so the oracle's edge decision is then reproduced up to
+// the fp64 arithmetic; for later bounces the fp32 ray itself, whose origin is the fp32 path's own hit point.
 #ifndef RT_QUAD_REFINE
 #define RT_QUAD_REFINE 1
 #endif
+// what quad_edge64 rebuilds the camera ray from: the path key and pixel (begin_sample), the bounce
+struct EdgeRay {
+  uint32_t ks, xy, bounce;
+};
+RT_EXT_FN bool quad_edge64(const Quad<double>* q64, const CamDev* cam, V<float> o, V<float> d, float tmin, float tmax,
+                           EdgeRay er) {
+  V<double> od = mkv((double)o.x, (double)o.y, (double)o.z), dd = mkv((double)d.x, (double)d.y, (double)d.z);
+  if (cam != nullptr && er.bounce == 0) {  // begin_sample's ray (camera.h:245-251, 293), same operations
+    const double ox = to_unit<double>(draw_u32(er.ks, 0)) - 0.5, oy = to_unit<double>(draw_u32(er.ks, 1)) - 0.5;
+    const double x = double(er.xy & 0xFFFFu), y = double(er.xy >> 16);
+    od = cam->pos;
+    dd = ((cam->dir00 + x * cam->du) + y * cam->dv + ox * cam->du) + oy * cam->dv;
+  }
+  const Quad<double>& q = *q64;
+  double t64;
+  return quad_test(ld3(q.n), q.D, ld3(q.q), ld3(q.a), ld3(q.b), od, dd, (double)tmin, (double)tmax, t64);
+}
+// the fp32 test with the near-edge re-decision: ref64(tmin, tmax) decides a near-edge hit (have64 false: none)
 template <class REF>
 __device__ __forceinline__ bool quad_test_near(V<float> n, float D, V<float> q, V<float> qa, V<float> qb, V<float> o,
                                                V<float> d, float tmin, float tmax, float& t, bool have64, REF ref64) {
@@ -533,10 +552,7 @@ __device__ __forceinline__ bool quad_test_near(V<float> n, float D, V<float> q, 
   const float a = dot(p, qa), b = dot(p, qb);
   const float m = fminf(fminf(fabsf(a), fabsf(a - 1.0f)), fminf(fabsf(b), fabsf(b - 1.0f)));
   if (have64 && m < 0x1p-12f) {
-    double t64;
-    if (!ref64(mkv((double)o.x, (double)o.y, (double)o.z), mkv((double)d.x, (double)d.y, (double)d.z), (double)tmin,
-               (double)tmax, t64))
-      return false;
+    if (!ref64(tmin, tmax)) return false;
     t = th;
     return true;
   }
@@ -548,15 +564,17 @@ template <class R>
 __device__ __forceinline__ bool quad_t(const Quad<R>& q, V<R> o, V<R> d, R tmin, R tmax, R& t) {
   return quad_test(ld3(q.n), q.D, ld3(q.q), ld3(q.a), ld3(q.b), o, d, tmin, tmax, t);
 }
-// quad i of the scene (binary BVH traversal); fp32 with the fp64 re-decision near an edge
+// quad i of the scene (binary BVH traversal); fp32 with the fp64 re-decision near an edge (`world`: the ray is in
+// world space, not an instance's object space, so a camera ray can be rebuilt in fp64)
 template <class R>
-__device__ __forceinline__ bool quad_t_near(const DevScene<R>& sc, uint32_t i, V<R> o, V<R> d, R tmin, R tmax, R& t) {
+__device__ __forceinline__ bool quad_t_near(const DevScene<R>& sc, uint32_t i, V<R> o, V<R> d, R tmin, R tmax, R& t,
+                                            EdgeRay er, bool world) {
   const Quad<R>& q = sc.quads[i];
   if constexpr (sizeof(R) == 4 && RT_QUAD_REFINE) {
     const Quad<double>* q64 = sc.quads64;
     return quad_test_near(ld3(q.n), q.D, ld3(q.q), ld3(q.a), ld3(q.b), o, d, tmin, tmax, t, q64 != nullptr,
-                          [&](V<double> od, V<double> dd, double t0, double t1, double& t64) {
-                            return quad_t(q64[i], od, dd, t0, t1, t64);
+                          [&](float t0, float t1) {
+                            return quad_edge64(q64 + i, world ? sc.cam64 : nullptr, o, d, t0, t1, er);
                           });
   }
   return quad_t(q, o, d, tmin, tmax, t);
@@ -695,15 +713,12 @@ __device__ __forceinline__ T ld_uniform(const T* p, uint32_t i) {
 // all of them). ld_uniform's constant-address-space load is turned back into per-lane vector loads
 // (global_load with a zero VGPR offset) in the large persistent kernels (round 3: the flat program's
 // record pairs, boxes and the linear program's records), each a VMEM issue and an L1 round trip.
-#ifndef RT_SCALAR_ASM
-#define RT_SCALAR_ASM 1
-#endif
 typedef uint32_t SRegs16 __attribute__((ext_vector_type(16)));
 typedef uint32_t SRegs8 __attribute__((ext_vector_type(8)));
 typedef uint32_t SRegs4 __attribute__((ext_vector_type(4)));
 template <class T>
 __device__ __forceinline__ T ld_scalar(const T* p) {
-#if defined(__HIP_DEVICE_COMPILE__) && RT_SCALAR_ASM
+#if defined(__HIP_DEVICE_COMPILE__)
   constexpr uint32_t n = sizeof(T) / 4;
   static_assert(sizeof(T) % 16 == 0 && n <= 32, "ld_scalar: 16-byte multiples up to 128 bytes");
   T t;
@@ -947,7 +962,7 @@ __device__ unsigned long long g_trace_totals[3];
 #endif
 template <class R, int STACK, int BLOCK>
 __device__ void trace(const DevScene<R>& sc, const Node<R>* nodes, V<R> wo, V<R> wd, R time, uint32_t excl_e,
-                      int32_t excl_i, Keys keys, uint32_t bounce, uint32_t* stk, R& t_best, uint32_t& e_best,
+                      int32_t excl_i, Keys keys, uint32_t bounce, uint32_t xy, uint32_t* stk, R& t_best, uint32_t& e_best,
                       int32_t& i_best) {
   const R tmin = R(0.001);
   R tmax = Num<R>::inf();
@@ -974,7 +989,7 @@ __device__ void trace(const DevScene<R>& sc, const Node<R>* nodes, V<R> wo, V<R>
     bool h;
     if (ty == E_QUAD) {
       if (self) return;
-      h = quad_t_near(sc, i, o, d, tmin, tmax, th);
+      h = quad_t_near(sc, i, o, d, tmin, tmax, th, EdgeRay{keys.ks, xy, bounce}, cur < 0);
     } else if (ty == E_SPHERE) {
       h = sphere_t(sc.spheres[i], o, d, time, tmin, tmax, self, th);
     } else {
@@ -1088,6 +1103,16 @@ __device__ void trace(const DevScene<R>& sc, const Node<R>* nodes, V<R> wo, V<R>
 // LDS copy of a node: 144-byte stride (36 dwords), so the 16 lanes of a ds_read_b128 group that
 // read 16 consecutive nodes hit 16 distinct 4-bank windows (a 128-byte stride gives 2).
 constexpr uint32_t kWNodeLdsStride = 144;
+// The LDS copy of the top of a tree in HBM (RT_WIDE_TOP, fp32 rays): a node's six plane rows and its child codes,
+// 112 bytes (28 banks) apart, so the 4-bank windows of 16 consecutive nodes are 16 distinct ones of the 64 banks.
+// The WNode stride of 128 bytes put every node's row r on one of only two windows: lanes reading the top of the
+// tree serialised on the banks (C4 fp32: 43 G bank-conflict cycles per launch against 93 G of LDS activity,
+// r05fin4_c4_f32_pmc.json).
+#ifndef RT_WIDE_TOP_STRIDE
+#define RT_WIDE_TOP_STRIDE 112
+#endif
+constexpr uint32_t kWTopStride = RT_WIDE_TOP_STRIDE;
+static_assert(kWTopStride == 112 || kWTopStride == 128, "a top node is its 7 rows, optionally padded to 8");
 #ifdef RT_SECTION_CLOCKS
 // development build (scripts/dev_wide_stats.py): wave-level counts of the wide kernels, per block
 // in LDS, added to g_wide_stats at the end: [0] node-loop iterations, [1] lanes in them, [2]
@@ -1217,9 +1242,9 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
   // Over a tree in HBM (C4 stand-in) the one bound culls too little: a ray with a small direction
   // component has a large o_a * inv_a, and the bound then widens every axis (C4 fp32 310.7 -> 378.5
   // ms/frame; C3 49.8 -> 48.8). RT_WIDE_FMA32=2: per-axis constants, as the fp64 rays'.
-  constexpr bool kFma = (F64 && RT_WIDE_FMA) || (!F64 && LDSN && RT_WIDE_FMA32 == 2);
+  constexpr bool kFma = (F64) || (!F64 && LDSN && RT_WIDE_FMA32 == 2);
   constexpr bool kFma32 = !F64 && LDSN && RT_WIDE_FMA32 == 1;
-  constexpr bool kOct = kFma || kFma32 || (!F64 && RT_WIDE_OCT32);
+  constexpr bool kOct = kFma || kFma32 || (!F64);
   [[maybe_unused]] const uint32_t onx0 = (__float_as_uint(inv.x) >> 31) * 48u,
                                  ony0 = 16u + (__float_as_uint(inv.y) >> 31) * 48u,
                                  onz0 = 32u + (__float_as_uint(inv.z) >> 31) * 48u;
@@ -1253,7 +1278,7 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
   // (a tree in HBM is addressed as its base plus a 32-bit byte offset, so each load is one global_load
   // with the base in SGPRs and the offset in one VGPR, not a 64-bit address per plane)
   // (RT_WIDE_OFS64: the fp64 kernels keep 64-bit addresses)
-  constexpr bool kOfs = LDSN || !F64 || !RT_WIDE_OFS64;
+  constexpr bool kOfs = LDSN || !F64;
   const unsigned char* nbase = LDSN ? lds_nodes : (const unsigned char*)sc.wnodes;
   using OfsT = typename std::conditional<kOfs, uint32_t, uint64_t>::type;
   auto node_off = [](uint32_t c) -> OfsT { return LDSN ? (OfsT)(c << 4) : (OfsT)c * (OfsT)sizeof(WNode); };
@@ -1272,7 +1297,7 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
     };
     if constexpr (kOct) {
       uint32_t onx = onx0, ony = ony0, onz = onz0;
-      if constexpr (RT_WIDE_OCTPACK) {
+      {  // (RT_WIDE_OCTPACK, always on)
         asm volatile("" : "+v"(oct));  // not loop-invariant to the compiler: unpacked here, per visit
         onx = oct & 0xFFu;
         ony = (oct >> 8) & 0xFFu;
@@ -1328,7 +1353,7 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
   // RT_WIDE_TOP (fp32 rays over a tree in HBM): nodes [0, wide_top) -- the first levels, which every ray
   // visits -- are read from the LDS copy the kernel made at its start (WideTrav::fill), so those visits
   // take no slot of the L1 address path, the C4 kernel's bound
-  constexpr bool kTopL = !LDSN && !F64 && RT_WIDE_TOP;
+  constexpr bool kTopL = !LDSN && !F64;
   [[maybe_unused]] const uint32_t ntop = kTopL ? min(sc.wide_top, (uint32_t)RT_WIDE_TOP_N) : 0u;
   // RT_WIDE_HALF_F64: the keys of node c from the tree's fp16 form (rt_scene.h WNodeH), and its child codes.
   // A plane's distance is one fma of its fp16 offset (v_fma_mix_f32): h * inv + b, b = (origin - o) *
@@ -1337,7 +1362,7 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
   // is culled; the fma's own rounding is relative, covered by box_slack like the float path's. The near
   // and far words of each axis are picked by v_perm_b32 with a per-ray selector (0x07060504: the hi
   // word, for a negative direction; 0x03020100: the lo word).
-  constexpr bool kHalf = !LDSN && F64 && RT_WIDE_HALF_F64;
+  constexpr bool kHalf = !LDSN && F64;
   [[maybe_unused]] const unsigned char* hbase = kHalf ? (const unsigned char*)sc.wnodesh : nullptr;
   [[maybe_unused]] const uint32_t selx = (__float_as_uint(inv.x) >> 31) ? 0x07060504u : 0x03020100u,
                                   sely = (__float_as_uint(inv.y) >> 31) ? 0x07060504u : 0x03020100u,
@@ -1410,7 +1435,7 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
       // a kernel with triangles loads a record's next two words with its first (the word stream is
       // padded, rt_scene.h), so a triangle costs one memory latency, not two: its kind is in word 0
       [[maybe_unused]] WW a1{}, a2{};
-      constexpr bool PF = TRI && RT_WIDE_PREFETCH;
+      constexpr bool PF = TRI;
       if constexpr (PF) {
         a1 = pw(w + 1);
         a2 = pw(w + 2);
@@ -1429,8 +1454,11 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
         hit = e != excl_e && tri_test(mkv(h.x, h.y, h.z), mkv(a.x, a.y, a.z), mkv(b.x, b.y, b.z), ro, rd, tmin, tmax, th);
       } else if (QUAD) {
         const WW nD = PF ? a1 : pw(w + 1), qa = PF ? a2 : pw(w + 2), qb = pw(w + 3);
-        // (no fp64 re-decision near edges here, unlike quad_t_near: its registers spilled the C4 fp32 kernel,
-        // 8 -> 104 B per lane, 264 -> 288 ms/frame, r05fin; the wide kernels with quads are the triangle ones)
+        // (no fp64 re-decision near edges here, unlike quad_t_near. Inline, its registers spilled the C4 fp32
+        // kernel: 8 -> 104 B per lane, 264 -> 288 ms/frame (r05fin). As a call (quad_edge64, round 6) the state
+        // saved around it spilled the kernel's loop instead: 264.6 -> 307.5 ms/frame, for a C4 lit fp32 RMSE
+        // (fp32 against fp64 over 400 tiles) of 1.71e-4 -> 1.30e-4 -- the rest are triangle edges and the
+        // fp32 paths' own rounding (r06a))
         hit = e != excl_e && quad_test(mkv(nD.x, nD.y, nD.z), nD.w, mkv(h.x, h.y, h.z), mkv(qa.x, qa.y, qa.z),
                                        mkv(qb.x, qb.y, qb.z), ro, rd, tmin, tmax, th);
         w += 4;
@@ -1444,7 +1472,7 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
   [[maybe_unused]] auto half_keys = [&](uint32_t c, uint32_t& k0, uint32_t& k1, uint32_t& k2, uint32_t& k3, uint4& cc) {
     half_keys_from(ldh_mem, c, k0, k1, k2, k3, cc);
   };
-  constexpr bool kTopH = kHalf && RT_WIDE_TOP_F64;
+  constexpr bool kTopH = kHalf;
   [[maybe_unused]] const uint32_t ntoph = kTopH ? min(sc.wide_top, (uint32_t)RT_WIDE_TOP_N_F64) : 0u;
   if (ry.fresh) {  // every lane alike: no divergence, and the tree starts bounded by their hit
     test_prims(0u, sc.wide_big);
@@ -1494,9 +1522,10 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
         } else if constexpr (kTopL) {
           nof = node_off(cur);
           if (cur < ntop) {
-            const float4 c4 = ld_top(nof + 96u);
+            const OfsT tof = cur * kWTopStride;
+            const float4 c4 = ld_top(tof + 96u);
             cc = make_uint4(__float_as_uint(c4.x), __float_as_uint(c4.y), __float_as_uint(c4.z), __float_as_uint(c4.w));
-            node_keys_from(ld_top, nof, k0, k1, k2, k3);
+            node_keys_from(ld_top, tof, k0, k1, k2, k3);
           } else {
             cc = *(const uint4*)(nbase + (nof + 96u));
             node_keys(nof, k0, k1, k2, k3);
@@ -2086,7 +2115,7 @@ __device__ __forceinline__ R light_pdf(const Light<R>* Lp, V<R> o, V<R> dir, boo
     R t;
     bool hit;
     const int32_t aligned = ld_here(&Lp->aligned);
-    if constexpr (sizeof(R) == 8 && RT_LIGHT_PDF_F64) {
+    if constexpr (sizeof(R) == 8) {
       if (aligned) {  // uniform branch
         const LightAF<R> af = ld_here(reinterpret_cast<const LightAF<R>*>(Lp->af));
         switch (aligned) {

@@ -46,33 +46,20 @@ using namespace rtd;
 namespace {
 
 constexpr int kBlock = 256;
-#ifndef RT_BG_BLACK_SKIP  // shade: no unit-sphere test for a miss against a solid black background
-#define RT_BG_BLACK_SKIP 1
-#endif
-#ifndef RT_BG_SOLID_FAST  // shade: nor against another solid background when |d| < 500 (the test always hits)
-#define RT_BG_SOLID_FAST 1
-#endif
-#ifndef RT_CAM_BASE
-#define RT_CAM_BASE 1
-#endif
+// RT_BG_BLACK_SKIP (retired in round 6, always on): shade: no unit-sphere test for a miss against a solid black
+// background
+// RT_BG_SOLID_FAST (retired in round 6, always on): shade: nor against another solid background when |d| < 500 (the
+// test always hits)
 #ifndef RT_LINEAR_WAVES
 #define RT_LINEAR_WAVES 6
 #endif
-#ifndef RT_SPHERE_REFINE  // fp32 sphere hits: point and normal from an fp64 re-solve (shade)
-#define RT_SPHERE_REFINE 1
-#endif
-#ifndef RT_COLD_LDS  // the volume linear program: the cold path state in LDS (Path, LC)
-#define RT_COLD_LDS 1
-#endif
-#ifndef RT_COLD_LDS_F64  // the same for the fp64 volume program (round 4)
-#define RT_COLD_LDS_F64 1
-#endif
-#ifndef RT_LINEAR_NORAD  // the volume programs: emission added straight into the item's running sum (Path NORAD)
-#define RT_LINEAR_NORAD 1
-#endif
-#ifndef RT_F64_TAIL  // 1: fp64 renders use the fp32 item layout (bulk + tail items); 0: uniform items of 16
-#define RT_F64_TAIL 1
-#endif
+// RT_SPHERE_REFINE (retired in round 6, always on): fp32 sphere hits: point and normal from an fp64 re-solve (shade)
+// RT_COLD_LDS (retired in round 6, always on): the volume linear program: the cold path state in LDS (Path, LC)
+// RT_COLD_LDS_F64 (retired in round 6, always on): the same for the fp64 volume program (round 4)
+// RT_LINEAR_NORAD (retired in round 6, always on): the volume programs: emission added straight into the item's running
+// sum (Path NORAD)
+// RT_F64_TAIL (retired in round 6, always on): 1: fp64 renders use the fp32 item layout (bulk + tail items); 0: uniform
+// items of 16
 #ifndef RT_PERSIST_MODE  // 2: dynamic (per-XCD heads), 1: static striding (development A/B)
 #define RT_PERSIST_MODE 2
 #endif
@@ -89,11 +76,14 @@ constexpr int kBlock = 256;
                              // 128 VGPRs) 1661 ms/frame, 5: 1567, 6: 2594 (spills); round 4 (cold state in LDS,
 #define RT_LINEAR_VOL_WAVES 6  // radiance folded, table sin/cos): 5: 1,326, 6: 1,247
 #endif
-#ifndef RT_LIN_LLI  // the volume program for lambertian + isotropic + light scenes (shade LL, LLI): C5 fp32
-#define RT_LIN_LLI 1  // 1,189 -> 1,124 ms/frame, fp64 2,358 -> 2,262 (r05y)
-#endif
-#ifndef RT_LINEAR_VOL_WAVES_LLI  // its fp32 form at 7 waves (79 VGPRs at 6): 1,124 -> 1,097 ms/frame (r05y); 8 (64
-#define RT_LINEAR_VOL_WAVES_LLI 8  // VGPRs + 60 B spilled): 1,098 -> 1,080 (r05v2). (C3 fp64 NL at 6 waves: 65.2 -> 69.5)
+// RT_LIN_LLI (retired in round 6, always on): the volume program for lambertian + isotropic + light scenes (shade LL,
+// LLI): C5 fp32 1,189 -> 1,124 ms/frame, fp64 2,358 -> 2,262 (r05y)
+// the LLI volume program's fp32 form at 7 waves per SIMD (72 VGPRs + 36 B spilled; 79 VGPRs at 6): 1,124 -> 1,097
+// ms/frame (r05y). 8 waves (64 VGPRs + 60 B spilled) was 1.6 % faster (r05v2; r06a 1,070 against 1,094 ms) but its
+// scratch -- 60 B for each of 8,192 waves' 64 lanes, 31 MB, about the L2s' size -- went to memory: 78.6 GB of writes
+// per launch (r06a PMC) against 2.2 GB at 7 waves, where the partial sums are ~1.2 GB. Round 6 keeps 7.
+#ifndef RT_LINEAR_VOL_WAVES_LLI
+#define RT_LINEAR_VOL_WAVES_LLI 7
 #endif
 #ifndef RT_LINEAR_VOL_WAVES_F64  // the fp64 volume program (round 4, cold state in LDS): 3 waves 2,672 ms/frame, 4: 2,400
 #define RT_LINEAR_VOL_WAVES_F64 4
@@ -129,6 +119,8 @@ constexpr uint32_t kItemsTarget = 4000000;
 // item partial sums of one pass at most (render(): a call needing more renders its chunks in passes)
 constexpr uint64_t kPartialBudget = 2ull << 30;
 constexpr uint32_t kMinAutoChunk = 2;
+constexpr double kItemFinalFrac = 0.0;  // (auto_final_frac)
+constexpr uint32_t kItemFinalChunk = 2;
 static uint32_t auto_chunk(bool flat) {
   return std::max(1u, flat ? env_u32("RT_ITEM_CHUNK_FLAT", 2 * kAutoChunk) : env_u32("RT_ITEM_CHUNK", kAutoChunk / 2));
 }
@@ -138,6 +130,9 @@ static uint32_t auto_tail_chunk(bool flat) {
 static double auto_tail_frac(bool flat) {
   return std::min(1.0, std::max(0.0, flat ? env_f64("RT_ITEM_TAIL_FRAC_FLAT", 0.125) : env_f64("RT_ITEM_TAIL_FRAC", 0.5)));
 }
+// the final tier of the layout: the last final_frac of every pixel's samples in items of final_chunk (render())
+static double auto_final_frac() { return std::min(1.0, std::max(0.0, env_f64("RT_ITEM_FINAL_FRAC", kItemFinalFrac))); }
+static uint32_t auto_final_chunk() { return std::max(1u, env_u32("RT_ITEM_FINAL_CHUNK", kItemFinalChunk)); }
 constexpr int kAutoSegments = 16;  // segments each slot advances per k_step launch
 // persistent schedule: upper bound of the grid's lanes. The dynamic schedule (persist 2) cuts the
 // grid to what the chip holds resident; the static one (persist 1) launches them all (~10x the
@@ -152,6 +147,8 @@ constexpr uint32_t kHeads = 8;
 constexpr uint32_t kHeadStride = 64;  // 256 B apart: one L2 line per head
 constexpr uint32_t kQBatch = 64;
 constexpr uint32_t kNoItem = 0xFFFFFFFFu;
+constexpr double kQueueTailLanes = 0.0;  // (launch_one)
+constexpr uint32_t kQueueTailBatch = 8;
 
 template <class R>
 struct alignas(4 * sizeof(R)) R4 {
@@ -165,19 +162,6 @@ struct alignas(4 * sizeof(R)) R4 {
 //   A  running sum of the item     S  key_pixel, key of the running sample, item, sample
 //   X  the surface the ray leaves (entry, instance): self-intersection exclusion;
 //      the pixel (x | y << 16) and the end of the sample range of the slot's item
-// The camera as camera::render/generate_ray use it (camera.h:137-141, 244-290), in double.
-struct CamDev {
-  int32_t mode;  // rt_camera_mode
-  int32_t pad;
-  V<double> pos, du, dv;
-  V<double> dir00;   // perspective / fisheye: f dir - vw/2 right + vh/2 up + (du + dv)/2 (camera.h:246, 260)
-  V<double> pos00;   // orthonormal / lens: pos - vw/2 right + vh/2 up + (du + dv)/2 (camera.h:253, 278)
-  V<double> dir;     // dir_, unit
-  V<double> fdir;    // focus_dist_ * dir_ (camera.h:279)
-  V<double> disk_u, disk_v;  // defocus_disk_u/v (camera.h:129-131)
-  double focal;      // focal_length_ (camera.h:266)
-};
-
 // utility.h:46-52 random_in_unit_disk by rejection; attempt k draws dimensions kDimDisk + 2k
 // and + 2k + 1 (far above the per-bounce dimensions); the origin after kDiskTries failures
 // (probability (1 - pi/4)^64 ~ 1e-43). Same as the oracle.
@@ -198,9 +182,10 @@ struct Params {
   const uint32_t* queue;   // live slots, or null = slots [0, n)
   uint32_t n;
   uint32_t P, npix, n_items, chunk, spp, first_sample, W;
-  // two item sizes: chunks [0, k_bulk) hold `chunk` samples, the later ones (the frame's last
-  // items in dequeue order) `tail_chunk` <= chunk samples each
-  uint32_t k_bulk, tail_chunk;
+  // up to three item sizes: chunks [0, k_bulk) hold `chunk` samples, the later ones (the frame's last
+  // items in dequeue order) `tail_chunk` <= chunk samples each, and from chunk k_fin on (the final tier;
+  // 0xFFFFFFFF: none) `fin_chunk` samples from sample fin_first on
+  uint32_t k_bulk, tail_chunk, k_fin, fin_chunk, fin_first;
   // the render's chunks come in passes (render(): the partial sums of one pass fit a memory budget): this
   // launch's items are chunks [chunk0, chunk0 + n_items / npix) of every pixel
   uint32_t chunk0;
@@ -218,6 +203,9 @@ struct Params {
   // the grid is what the chip holds resident and lanes pull items from the per-XCD heads
   int32_t persist;
   uint32_t* heads;  // kHeads dequeue counters, kHeadStride words apart (persist 2)
+  // persist 2: items [0, q_split) are handed out in batches of kQBatch, the frame's last items [q_split,
+  // n_items) in batches of q_tbatch (launch_one; q_split is a multiple of kHeads * kQBatch)
+  uint32_t q_split, q_tbatch;
   uint64_t seg_cap;  // a lane never needs more segments than this (its items * chunk * max_depth)
   uint32_t* fault;   // set when a lane hits seg_cap (internal error, reported by the host)
 };
@@ -261,9 +249,7 @@ struct Path {
   // cold state (register copies: unused when LC)
   V<R> acc_;
   uint32_t ka_, item_, sample_, send_, xy_;
-#if RT_CAM_BASE
   V<double> cb_;  // (dir00 + x du) + y dv of the item's pixel (pixel_base)
-#endif
 #ifdef RT_ITEM_CLOCKS
   uint64_t t0_;  // development: wall clock at the item's start
 #endif
@@ -304,7 +290,6 @@ struct Path {
   RT_COLD_U32(send, kSend)
   RT_COLD_U32(xy, kXy)
 #undef RT_COLD_U32
-#if RT_CAM_BASE
   __device__ __forceinline__ V<double> cb() const {
     if constexpr (LC) return mkv(cold_doubles()[0], cold_doubles()[kBlock], cold_doubles()[2 * kBlock]);
     else return cb_;
@@ -318,7 +303,6 @@ struct Path {
       cb_ = v;
     }
   }
-#endif
 };
 static_assert(Path<float>::kXy < kColdWords, "cold words");
 
@@ -327,12 +311,10 @@ static_assert(Path<float>::kXy < kColdWords, "cold words");
 // launch), not once per sample. Same operations in the same order: bit-identical.
 template <class R, class PS>
 __device__ __forceinline__ void pixel_base(const Params<R>& p, PS& s, uint32_t xy) {
-#if RT_CAM_BASE
   if constexpr (!PS::kLean) {
     const double x = double(xy & 0xFFFFu), y = double(xy >> 16);
     s.set_cb((ld_here(&p.camx->dir00) + x * ld_here(&p.camx->du)) + y * ld_here(&p.camx->dv));
   }
-#endif
 }
 
 template <class R>
@@ -377,16 +359,21 @@ __device__ __forceinline__ uint32_t* wave_queue() {
   return wq + 2 * (threadIdx.x >> 6);
 }
 
-// A batch of kQBatch items for the calling lane's wave: the block's own head first (blocks b and
-// b + 8 share an XCD, so a head's counter stays in one XCD's traffic), then the others. Returns the
-// first item, or kNoItem once every head has run past the item space.
-__device__ __forceinline__ uint32_t grab_batch(uint32_t* heads, uint32_t n_items) {
+// A batch of items for the calling lane's wave: the block's own head first (blocks b and b + 8 share an
+// XCD, so a head's counter stays in one XCD's traffic), then the others. Ticket j of head h is batch j *
+// kHeads + h of kQBatch items while j < q_split / (kHeads * kQBatch); the tickets after those are batches of
+// q_tbatch items over [q_split, n_items), numbered the same way. Returns the first item, or kNoItem once
+// every head has run past the item space.
+template <class R>
+__device__ __forceinline__ uint32_t grab_batch(const Params<R>& p) {
   const uint32_t g = blockIdx.x & (kHeads - 1);
+  const uint32_t ja = p.q_split / (kHeads * kQBatch);
   for (uint32_t t = 0; t < kHeads; t++) {
     const uint32_t h = (g + t) & (kHeads - 1);
-    const uint32_t j = atomicAdd(heads + h * kHeadStride, 1u);
-    const uint64_t first = ((uint64_t)j * kHeads + h) * kQBatch;
-    if (first < n_items) return (uint32_t)first;
+    const uint32_t j = atomicAdd(p.heads + h * kHeadStride, 1u);
+    const uint64_t first = j < ja ? ((uint64_t)j * kHeads + h) * kQBatch
+                                  : p.q_split + ((uint64_t)(j - ja) * kHeads + h) * p.q_tbatch;
+    if (first < p.n_items) return (uint32_t)first;
   }
   return kNoItem;
 }
@@ -414,14 +401,14 @@ __device__ __forceinline__ uint32_t next_item_dyn(const Params<R>& p) {
     off += take;
     if (off >= k || qe == kNoItem) break;  // served, or the wave already found every head dry
     uint32_t b = kNoItem;
-    if (lane == leader) b = grab_batch(p.heads, p.n_items);
+    if (lane == leader) b = grab_batch(p);
     b = __shfl(b, (int)leader);
     if (b == kNoItem) {  // remember it: a dry scan stalls the wave for kHeads atomics
       qn = qe = kNoItem;
       break;
     }
     qn = b;
-    qe = min(b + kQBatch, p.n_items);
+    qe = min(b + (b < p.q_split ? kQBatch : p.q_tbatch), p.n_items);
   }
   if (lane == leader) {
     __hip_atomic_store(wq, qn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
@@ -440,9 +427,10 @@ __device__ __forceinline__ void item_range(const Params<R>& p, uint32_t item, ui
   const uint32_t chunk = lchunk + p.chunk0;
   // fp64 items are uniform (the host never gives them a tail): compiled out, the select costs
   // the fp64 Cornell kernel 10 VGPRs, 3 -> 2 waves per SIMD (C2 f64 5.22 -> 4.08 Gsamples/s)
-  const bool bulk = (sizeof(R) == 8 && !RT_F64_TAIL) || chunk < p.k_bulk;
-  first = bulk ? chunk * p.chunk : p.k_bulk * p.chunk + (chunk - p.k_bulk) * p.tail_chunk;
-  end = min(first + (bulk ? p.chunk : p.tail_chunk), p.spp);
+  const bool bulk = chunk < p.k_bulk, fin = chunk >= p.k_fin;
+  first = bulk ? chunk * p.chunk
+               : (fin ? p.fin_first + (chunk - p.k_fin) * p.fin_chunk : p.k_bulk * p.chunk + (chunk - p.k_bulk) * p.tail_chunk);
+  end = min(first + (bulk ? p.chunk : (fin ? p.fin_chunk : p.tail_chunk)), p.spp);
 }
 // the pixel's RNG key and the end of the item's samples: kept, or (LEAN) recomputed
 template <class R, class PS>
@@ -544,7 +532,7 @@ __device__ __forceinline__ void begin_sample(const Params<R>& p, PS& s) {
   double tm;
   if (!CAMX || p.cam_mode == RT_CAM_PERSPECTIVE) {  // camera.h:245-251
     const V<double> du = ld_here(&p.camx->du), dv = ld_here(&p.camx->dv);
-    if constexpr (RT_CAM_BASE && !PS::kLean) {
+    if constexpr (!PS::kLean) {
       d = (s.cb() + ox * du) + oy * dv;
     } else {  // the same operations in the same order as pixel_base + the above: bit-identical
       const uint32_t xy = s.xy(), x = xy & 0xFFFFu, y = xy >> 16;
@@ -621,13 +609,15 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
     // a solid black background (the Cornell configs' solid_color::black) adds thr * 0: the unit-sphere test
     // that decides whether it is sampled (camera.h:183-187) is skipped (a wave-uniform test of the record)
     const Texture<R>* bgt = sc.background >= 0 ? sc.texs + sc.background : nullptr;
-    const bool bg_black = RT_BG_BLACK_SKIP && bgt != nullptr && ld_here(&bgt->kind) == T_SOLID &&
+    const bool bg_black = bgt != nullptr && ld_here(&bgt->kind) == T_SOLID &&
                           ld_here(&bgt->c0[0]) == R(0) && ld_here(&bgt->c0[1]) == R(0) && ld_here(&bgt->c0[2]) == R(0);
     // any other solid background: the unit sphere about the ray's origin has the root t = 1/|d|, inside
     // [0.001, inf) for |d| < 1000, and a solid colour does not depend on where it is hit -- so for |d| < 500
     // the colour is added without the test (RT_BG_SOLID_FAST; RTOW's sky, C3)
-    const bool bg_solid = RT_BG_SOLID_FAST && bgt != nullptr && !bg_black && ld_here(&bgt->kind) == T_SOLID &&
-                          dot(d, d) < R(250000);
+    // (0 < |d|^2: a zero direction has a = 0 in sphere.h:48-62, a NaN root and no hit -- nothing is added)
+    const R dd2 = dot(d, d);
+    const bool bg_solid = bgt != nullptr && !bg_black && ld_here(&bgt->kind) == T_SOLID &&
+                          dd2 < R(250000) && dd2 > R(0);
     if (bg_solid) {
       add = s.thr * mkv(ld_here(&bgt->c0[0]), ld_here(&bgt->c0[1]), ld_here(&bgt->c0[2]));
       has_add = true;
@@ -695,7 +685,6 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
         if constexpr (sizeof(R) == 8) {
           outward = (po - ld3(sp.cn)) / sp.r;
         } else {
-#if RT_SPHERE_REFINE
           // The hit refined in fp64 from the fp32 ray: one Newton step on the quadratic
           // g(t) = a t^2 + 2 b t + c from the fp32 root (which is ~1e-7 relative off: ~1e-6 along
           // the ray for t ~ 10, tilting a small sphere's normal by ~1e-5 -- enough for a chain of
@@ -720,9 +709,6 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
           const double px = ox + td * dx, py = oy + td * dy, pz = oz + td * dz;
           po = mkv((float)px, (float)py, (float)pz);
           outward = mkv((float)(px - sp.cn[0]), (float)(py - sp.cn[1]), (float)(pz - sp.cn[2])) * fdiv(R(1), sp.r);
-#else
-          outward = (po - ld3(sp.cn)) * fdiv(R(1), sp.r);
-#endif
           // big spheres (the RTOW ground, r = 1000) in particular: o + t*d in fp32 is off the surface
           // by ~1e-7 absolute, enough to flip the sign of y near the top of the ground (y = 0 under the
           // glass sphere) and with it the checker parity (texture.h:51-55)
@@ -960,9 +946,9 @@ struct LinearTrav {
   static constexpr bool kWide = false;
   // the volume program's registers (C5: 23 -> 6 VGPRs spilled at 96, 1563 -> 1498 ms/frame)
   static constexpr bool kTablesLds = false;
-  static constexpr bool kLean = false;
-  static constexpr bool kNoRad = VOL && RT_LINEAR_NORAD;
-  static constexpr bool kColdLds = VOL && (sizeof(R) == 4 ? RT_COLD_LDS : RT_COLD_LDS_F64);
+  static constexpr bool kLean = false;  // (LLI lean: 7 waves 1,094 -> 1,117 ms/frame; 8 waves 48 B spilled, r06a)
+  static constexpr bool kNoRad = VOL;
+  static constexpr bool kColdLds = VOL;
   template <class PS>
   __device__ __forceinline__ static void run(const DevScene<R>& sc, const Node<R>*, const PS& s, Keys k,
                                              uint32_t*, R& t, uint32_t& e, int32_t& i, uint32_t&) {
@@ -973,22 +959,16 @@ struct LinearTrav {
 #ifndef RT_FLAT_WAVES
 #define RT_FLAT_WAVES 8
 #endif
-#ifndef RT_F64_COLD_LDS  // fp64 flat program: the cold path state (item sum, pixel, keys, camera base) in LDS
-#define RT_F64_COLD_LDS 1
-#endif
-#ifndef RT_FLAT_LDS  // flat program (persistent kernels): records and materials copied into LDS
-#define RT_FLAT_LDS 1
-#endif
+// RT_F64_COLD_LDS (retired in round 6, always on): fp64 flat program: the cold path state (item sum, pixel, keys,
+// camera base) in LDS
+// RT_FLAT_LDS (retired in round 6, always on): flat program (persistent kernels): records and materials copied into LDS
 #ifndef RT_FLAT_WAVES_F64_LL  // the same for the lambertian + light kernel
 #define RT_FLAT_WAVES_F64_LL 7  // C2 fp64: 5 waves 28.90 ms/frame, 6: 28.08 (r05c; the general kernel at 5: 31.28);
                                 // 7 (72 VGPRs + 32 B spilled, from 80): 27.94 -> 27.79 (r05w7); 8 does not fit
 #endif
-#ifndef RT_FLAT_LL  // flat program: a kernel for lambertian + light scenes (shade LL)
-#define RT_FLAT_LL 1
-#endif
-#ifndef RT_FLAT_NORAD  // flat program: emission added straight into the item's running sum (Path NORAD)
-#define RT_FLAT_NORAD 1
-#endif
+// RT_FLAT_LL (retired in round 6, always on): flat program: a kernel for lambertian + light scenes (shade LL)
+// RT_FLAT_NORAD (retired in round 6, always on): flat program: emission added straight into the item's running sum
+// (Path NORAD)
 #ifndef RT_FLAT_WAVES_F64  // fp64 flat program: waves per SIMD the register budget is cut for (1: none)
 #define RT_FLAT_WAVES_F64 5
 #endif
@@ -1004,8 +984,8 @@ struct FlatTrav {
   static constexpr bool kWide = false;
   // fp32: 72 -> 64 VGPRs, but C2 23.5 -> 24.1 ms/frame; fp64: see RT_F64_COLD_LDS
   static constexpr bool kLean = false;
-  static constexpr bool kNoRad = RT_FLAT_NORAD;  // 6 VGPRs in fp64 (its item sum is in LDS)
-  static constexpr bool kColdLds = sizeof(R) == 8 && RT_F64_COLD_LDS;
+  static constexpr bool kNoRad = true;  // 6 VGPRs in fp64 (its item sum is in LDS)
+  static constexpr bool kColdLds = sizeof(R) == 8;
   template <class PS>
   __device__ __forceinline__ static void run(const DevScene<R>& sc, const Node<R>*, const PS& s, Keys, uint32_t*,
                                              R& t, uint32_t& e, int32_t& i, uint32_t& nm) {
@@ -1063,8 +1043,8 @@ struct StackTrav {
   template <class PS>
   __device__ __forceinline__ static void run(const DevScene<R>& sc, const Node<R>* nodes, const PS& s, Keys k,
                                              uint32_t* stk, R& t, uint32_t& e, int32_t& i, uint32_t&) {
-    trace<R, STACK, kBlock>(sc, LDSN ? nodes : sc.nodes, s.o, s.d, s.tm, s.xe, s.xi, k, (uint32_t)s.bounce, stk,
-                            t, e, i);
+    trace<R, STACK, kBlock>(sc, LDSN ? nodes : sc.nodes, s.o, s.d, s.tm, s.xe, s.xi, k, (uint32_t)s.bounce, s.xy(),
+                            stk, t, e, i);
   }
 };
 
@@ -1079,15 +1059,11 @@ struct StackTrav {
 // speculative traversal 5: 424, 6: 412.5 -- 7 blocks of 24 KB stacks do not fit the 160 KB LDS)
 #define RT_WIDE_WAVES_GLOBAL 8  // round 5, with 12 LDS stack entries and 55 top nodes in LDS (wide_lds_stack)
 #endif
-#ifndef RT_WIDE_TRIQUAD  // a kernel for triangle + quad scenes (else the all-kinds kernel): C4 358.9 -> 353.8 ms
-#define RT_WIDE_TRIQUAD 1
-#endif
-#ifndef RT_PARAM_RELOAD  // flat / linear / binary-BVH loops: parameters reloaded per segment
-#define RT_PARAM_RELOAD 1
-#endif
-#ifndef RT_WIDE_RELOAD
-#define RT_WIDE_RELOAD 1  // round 4 (lean state): C3 fp32 51.9 -> 51.1 ms/frame, fp64 71.3 -> 70.7, C4 neutral
-#endif
+// RT_WIDE_TRIQUAD (retired in round 6, always on): a kernel for triangle + quad scenes (else the all-kinds kernel): C4
+// 358.9 -> 353.8 ms
+// RT_PARAM_RELOAD (retired in round 6, always on): flat / linear / binary-BVH loops: parameters reloaded per segment
+// RT_WIDE_RELOAD (retired in round 6, always on): round 4 (lean state): C3 fp32 51.9 -> 51.1 ms/frame, fp64 71.3 ->
+// 70.7, C4 neutral
 #ifndef RT_SHADE_BATCH  // < 64: a wave stops traversing to shade once this many of its lanes have finished
 #define RT_SHADE_BATCH 48  // (LDS-resident tree, C3 fp32 ms/frame: never 57.06, 48: 52.57, 52: 52.58, 56: 52.81, 60: 53.57; fp64 81.3 -> 75.8)
 #endif
@@ -1106,15 +1082,9 @@ struct StackTrav {
 #ifndef RT_WIDE_WAVES_F64_NL  // the NL form over an LDS tree, fp64 (116 VGPRs at 4 waves)
 #define RT_WIDE_WAVES_F64_NL 5  // C3 fp64 at 4 waves 69.07 ms/frame, 5: 65.41 (r05q; the general kernel at 4: 70.23)
 #endif
-#ifndef RT_WIDE_NL  // a wide kernel for sphere scenes without a light (shade NL)
-#define RT_WIDE_NL 1
-#endif
-#ifndef RT_WIDE_LL  // a wide kernel for lambertian + light triangle/quad scenes (shade LL)
-#define RT_WIDE_LL 1
-#endif
-#ifndef RT_WIDE_LEAN  // the wide kernels keep the lean path state (Path LEAN)
-#define RT_WIDE_LEAN 1
-#endif
+// RT_WIDE_NL (retired in round 6, always on): a wide kernel for sphere scenes without a light (shade NL)
+// RT_WIDE_LL (retired in round 6, always on): a wide kernel for lambertian + light triangle/quad scenes (shade LL)
+// RT_WIDE_LEAN (retired in round 6, always on): the wide kernels keep the lean path state (Path LEAN)
 // LL: a lambertian + light scene (shade LL; the material table `Lm` in static LDS)
 template <class R, bool SPH, bool TRI, bool QUAD, bool MOV, bool LDSN, bool LL = false, bool NL = false>
 struct WideTrav {
@@ -1131,8 +1101,8 @@ struct WideTrav {
   static constexpr bool kWide = true;
   static constexpr bool kColdLds = false;  // its LDS holds the tree and the stacks
   static constexpr bool kTablesLds = false;
-  static constexpr bool kLean = RT_WIDE_LEAN;  // registers for the traversal (fewer spills)
-  static constexpr bool kNoRad = RT_WIDE_LEAN;
+  static constexpr bool kLean = true;  // registers for the traversal (fewer spills)
+  static constexpr bool kNoRad = true;
   static constexpr bool kMoving = MOV;
   using StackT = WStackT<LDSN>;
   using WW = typename WWord<R>::T;
@@ -1141,8 +1111,8 @@ struct WideTrav {
     return LDSN ? n_wnodes * kWNodeLdsStride + n_words * (uint32_t)sizeof(WW) : 0u;
   }
   // a tree in HBM, fp32 rays (RT_WIDE_TOP): [stack][the first wide_top nodes, WNode layout]
-  static constexpr bool kTop = !LDSN && sizeof(R) == 4 && RT_WIDE_TOP;
-  static constexpr bool kTopH = !LDSN && sizeof(R) == 8 && RT_WIDE_HALF_F64 && RT_WIDE_TOP_F64;
+  static constexpr bool kTop = !LDSN && sizeof(R) == 4;
+  static constexpr bool kTopH = !LDSN && sizeof(R) == 8;
   __host__ __device__ static uint32_t top_offset(uint32_t wide_stack) {
     return (wide_stack < wide_lds_stack<R>() ? wide_stack : wide_lds_stack<R>()) * kBlock * 4u;
   }
@@ -1170,7 +1140,11 @@ struct WideTrav {
       uint4* dst = (uint4*)(base + top_offset(sc.wide_stack));
       const uint4* gn = (const uint4*)sc.wnodes;
       const uint32_t ntop = min(sc.wide_top, (uint32_t)RT_WIDE_TOP_N);
-      for (uint32_t j = threadIdx.x; j < ntop * 8u; j += kBlock) dst[j] = gn[j];
+      constexpr uint32_t kRows = kWTopStride / 16u;  // 7: the pad row of WNode is not copied
+      for (uint32_t j = threadIdx.x; j < ntop * kRows; j += kBlock) {
+        const uint32_t nd = j / kRows, r = j - nd * kRows;
+        dst[j] = gn[nd * 8u + r];
+      }
       __syncthreads();
     } else if constexpr (kTopH) {  // fp64 rays: the fp16 form, 5 words per node
       uint4* dst = (uint4*)(base + top_offset(sc.wide_stack));
@@ -1351,19 +1325,13 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
       using StackT = typename Trav::StackT;
       const uint32_t root = Trav::root(p.sc);
       WideRayT<R> ry{root, 0, Num<R>::inf(), kNoHit, 1u};
-#if RT_WIDE_RELOAD
       using KP = const __attribute__((address_space(4))) Params<R>*;
       const KP kp0 = (KP)__builtin_amdgcn_kernarg_segment_ptr();
-#endif
 #pragma unroll 1
       for (;;) {
-#if RT_WIDE_RELOAD
         KP kp = kp0;
         asm volatile("" : "+s"(kp));
         const Params<R>& q = *(const Params<R>*)kp;
-#else
-        const Params<R>& q = p;  // (reloading q per segment as below: C3 1.5 % slower at 6 waves)
-#endif
 #ifdef RT_SECTION_CLOCKS
         const uint64_t c0 = clock64();
         const bool fin = Trav::steps(q.sc, trav_nodes, s, (StackT*)wstk, ry);
@@ -1412,23 +1380,17 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
         if (!shade<R, CAMX, true, true, true, Trav::kLL>(q, s, t, e, inst, nm, flat_tb->m, flat_tb->lm)) break;
       }
     } else {
-#if RT_PARAM_RELOAD
       // The parameters are read from the kernarg segment afresh each segment (the asm hides
       // the pointer from loop-invariant hoisting): hoisted, they outgrow the SGPR file and spill
       // into VGPR lanes, one v_readlane per use (C2 flat program: 73 SGPR spills -> 0, 24.9 ->
       // 23.9 ms/frame; scalar loads hit the constant cache)
       using KP = const __attribute__((address_space(4))) Params<R>*;
       const KP kp0 = (KP)__builtin_amdgcn_kernarg_segment_ptr();
-#endif
 #pragma unroll 1
       for (;;) {
-#if RT_PARAM_RELOAD
         KP kp = kp0;
         asm volatile("" : "+s"(kp));
         const Params<R>& q = *(const Params<R>*)kp;
-#else
-        const Params<R>& q = p;
-#endif
         R t;
         uint32_t e, nm = 0;
         int32_t inst;
@@ -1855,6 +1817,10 @@ uint32_t resident_blocks(const void* kern, int dev, size_t lds) {
   return r;
 }
 
+// The dynamic schedule's tail (launch_one): the last RT_QTAIL_LANES x (grid lanes) items of a launch are handed
+// out in batches of RT_QTAIL_BATCH items instead of kQBatch
+static double queue_tail_lanes() { return std::max(0.0, env_f64("RT_QTAIL_LANES", kQueueTailLanes)); }
+static uint32_t queue_tail_batch() { return env_u32("RT_QTAIL_BATCH", kQueueTailBatch); }
 // lanes of the last persistent launch on this host thread (rt_counters.grid_lanes)
 thread_local uint64_t t_grid_lanes = 0;
 
@@ -1866,6 +1832,11 @@ void launch_one(KernelT kern, Params<R> p, uint32_t grid, hipStream_t st, size_t
     if (res > 0) grid = std::min<uint32_t>(grid, res);
     p.P = grid * kBlock;
     p.seg_cap = (uint64_t)p.n_items * p.chunk * (uint64_t)p.max_depth + 1;
+    // the frame's last items in small batches, so that a wave does not hold a batch of them queued while
+    // lanes of other waves run dry (the tail of a short frame: one rank of eight)
+    const uint64_t tail = std::min<uint64_t>(p.n_items, (uint64_t)(queue_tail_lanes() * p.P));
+    p.q_split = (uint32_t)((p.n_items - tail) / (kHeads * kQBatch) * (kHeads * kQBatch));
+    p.q_tbatch = p.q_split < p.n_items ? std::max<uint32_t>(1u, std::min(kQBatch, queue_tail_batch())) : kQBatch;
   } else if (p.persist) {  // the lanes stride over the items by the grid's lane count
     p.P = grid * kBlock;
     p.seg_cap = ((uint64_t)p.n_items + p.P - 1) / p.P * p.chunk * (uint64_t)p.max_depth + 1;
@@ -1876,15 +1847,24 @@ void launch_one(KernelT kern, Params<R> p, uint32_t grid, hipStream_t st, size_t
 
 // Dynamic LDS of a wide-BVH launch: the whole tree when it fits the budget (LDSN), else the stack only.
 constexpr size_t kWideLdsBudget = 40u << 10;  // bytes per 256-lane block: 4 blocks per CU of 160 KiB
+// The fp32 kernel over a tree in HBM runs RT_WIDE_WAVES_GLOBAL blocks per CU only if that many blocks' LDS -- the
+// stack entries kept in LDS, the top of the tree and the small static tables -- fit the CU's 160 KiB. A knob
+// combination over it does not fail: the occupancy query quietly launches fewer blocks (the round-5 sweep's "24 /
+// 21 / 6" point ran at 5 blocks per CU), so it is refused here.
+static_assert(((size_t)RT_WIDE_LDS_STACK * kBlock * 4u + (size_t)RT_WIDE_TOP_N * kWTopStride + 1024u) *
+                      RT_WIDE_WAVES_GLOBAL <= (160u << 10),
+              "RT_WIDE_LDS_STACK / RT_WIDE_TOP_N do not fit RT_WIDE_WAVES_GLOBAL blocks per CU");
+static_assert(RT_WIDE_TOP_N <= kWideTopMax && RT_WIDE_TOP_N_F64 <= kWideTopMax,
+              "the scene compiler orders at most kWideTopMax top nodes first");
 template <class R>
 inline size_t wide_lds_bytes(const DevScene<R>& sc, bool ldsn) {
   // an LDS tree: every entry in LDS, uint16; a tree in HBM: up to wide_lds_stack uint32 entries (the rest spill)
   const size_t stack = ldsn ? (size_t)sc.wide_stack * kBlock * 2u
                             : (size_t)std::min<uint32_t>(sc.wide_stack, wide_lds_stack<R>()) * kBlock * 4u;
   // fp32 rays over a tree in HBM: the copy of its first levels (RT_WIDE_TOP)
-  const size_t top = (!ldsn && sizeof(R) == 4 && RT_WIDE_TOP)
-                         ? (size_t)std::min<uint32_t>(sc.wide_top, RT_WIDE_TOP_N) * sizeof(WNode)
-                     : (!ldsn && sizeof(R) == 8 && RT_WIDE_HALF_F64 && RT_WIDE_TOP_F64)
+  const size_t top = (!ldsn && sizeof(R) == 4)
+                         ? (size_t)std::min<uint32_t>(sc.wide_top, RT_WIDE_TOP_N) * kWTopStride
+                     : (!ldsn && sizeof(R) == 8)
                          ? (size_t)std::min<uint32_t>(sc.wide_top, RT_WIDE_TOP_N_F64) * sizeof(WNodeH) : 0u;
   return (ldsn ? (size_t)sc.n_wnodes * kWNodeLdsStride + (size_t)sc.n_wprim_words * sizeof(typename WWord<R>::T) : 0u) +
          stack + top;
@@ -1907,15 +1887,15 @@ void launch_wide_k(const Params<R>& p, uint32_t grid, hipStream_t st) {
 template <class R>
 inline void launch_wide(const Params<R>& p, bool ll, bool nl, uint32_t grid, hipStream_t st) {
   const uint32_t k = p.sc.wide_kinds;
-  if (k == WK_SPHERE && RT_WIDE_NL && nl)  // RTOW (C3)
+  if (k == WK_SPHERE && nl)  // RTOW (C3)
     launch_wide_k<R, true, false, false, false, false, true>(p, grid, st);
   else if (k == WK_SPHERE)
     launch_wide_k<R, true, false, false, false>(p, grid, st);
   else if (k == WK_TRI)
     launch_wide_k<R, false, true, false, false>(p, grid, st);
-  else if (RT_WIDE_TRIQUAD && k == (WK_TRI | WK_QUAD) && RT_WIDE_LL && ll && p.sc.n_mats <= 16)
+  else if (k == (WK_TRI | WK_QUAD) && ll && p.sc.n_mats <= 16)
     launch_wide_k<R, false, true, true, false, true>(p, grid, st);  // ... lambertian + light (the C4 stand-in)
-  else if (RT_WIDE_TRIQUAD && k == (WK_TRI | WK_QUAD))  // a mesh under a quad light
+  else if (k == (WK_TRI | WK_QUAD))  // a mesh under a quad light
     launch_wide_k<R, false, true, true, false>(p, grid, st);
   else
     launch_wide_k<R, true, true, true, true>(p, grid, st);
@@ -2003,8 +1983,8 @@ void launch_step(const Params<R>& p, KernelFamily fam, bool ll, bool nl, bool ll
   switch (fam) {
     case KF_FLAT:
       if constexpr (family_built(KF_FLAT)) {
-        if (RT_FLAT_LDS && p.persist && FlatTrav<R, true>::tables_fit(p.sc)) {
-          if (RT_FLAT_LL && ll && FlatTrav<R, true, true>::tables_fit(p.sc))
+        if (p.persist && FlatTrav<R, true>::tables_fit(p.sc)) {
+          if (ll && FlatTrav<R, true, true>::tables_fit(p.sc))
             launch_k<R, FlatTrav<R, true, true>>(p, grid, st);
           else
             launch_k<R, FlatTrav<R, true>>(p, grid, st);
@@ -2018,7 +1998,10 @@ void launch_step(const Params<R>& p, KernelFamily fam, bool ll, bool nl, bool ll
       return;
     case KF_LIN_VOL:
       if constexpr (family_built(KF_LIN_VOL)) {
-        if (RT_LIN_LLI && lli && p.sc.n_mats <= 16)  // lambertian + isotropic + light (C5)
+        // lambertian + isotropic + light (C5), persistent schedule only: the LLI form's shade and LDS material table
+        // are persist_body's; step_body (segments_per_launch > 0) shades with the general program, which its
+        // register budget would squeeze
+        if (lli && p.persist && p.sc.n_mats <= 16)
           launch_k<R, LinearTrav<R, false, false, true, true>>(p, grid, st);
         else
           launch_k<R, LinearTrav<R, false, false, true>>(p, grid, st);
@@ -2101,10 +2084,10 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     const uint32_t spp = (uint32_t)prm->spp;
     // the flat program's items are cheaper per sample, so its default items are twice as long
     // (fewer item ends, dequeues and partial-sum stores; C2: 23.9 -> 23.5 ms/frame)
-    const bool flat_prog = (!f64 || RT_F64_TAIL) && hdr.has_flat && prm->traversal != RT_TRAV_ORDERED &&
+    const bool flat_prog = hdr.has_flat && prm->traversal != RT_TRAV_ORDERED &&
                            make_view(cam).mode == RT_CAM_PERSPECTIVE && !(hdr.n_texdata > 0 || hdr.has_cell_noise);
     uint32_t chunk0 = prm->samples_per_item > 0 ? std::min<uint32_t>((uint32_t)prm->samples_per_item, spp)
-                                               : std::min<uint32_t>((f64 && !RT_F64_TAIL) ? kAutoChunk : auto_chunk(flat_prog), spp);
+                                               : std::min<uint32_t>(auto_chunk(flat_prog), spp);
     // a small frame (C1: 160,000 px x 64 spp is ~2 items of 16 per resident lane) takes smaller items, so
     // the lanes that finish early find work while the last items run: the automatic size is halved until
     // the whole frame has kItemsTarget items (the full image's pixels, not this call's tiles: the layout,
@@ -2120,16 +2103,27 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     // items of tail_chunk samples; both depend on spp alone, so the image is the same for any
     // tiling or rank count.
     uint32_t chunk = chunk0, tail_chunk = chunk0, k_bulk = (spp + chunk0 - 1) / chunk0, nchunks = k_bulk;
-    if (prm->samples_per_item <= 0 && (!f64 || RT_F64_TAIL)) {  // fp64: uniform items of 16 (C2 f64 with the fp32
-                                                // layout: 5.22 -> 4.04 Gsamples/s)
+    uint32_t k_fin = 0xFFFFFFFFu, fin_chunk = chunk0, fin_first = spp;
+    if (prm->samples_per_item <= 0) {  // (fp64 too since round 3: round 2 kept uniform items of 16 for it)
       const uint32_t ts = std::min<uint32_t>(spp, (uint32_t)((double)spp * auto_tail_frac(flat_prog) + 0.5));
+      // the final tier (RT_ITEM_FINAL_FRAC > 0): the last fs samples of the tail in items of fin_chunk
+      const uint32_t fs = std::min<uint32_t>(ts, (uint32_t)((double)spp * auto_final_frac() + 0.5));
       tail_chunk = std::min(chunk, auto_tail_chunk(flat_prog));
+      fin_chunk = std::min(tail_chunk, auto_final_chunk());
       for (;;) {
         k_bulk = (spp - ts) / chunk;  // bulk items cover [0, k_bulk * chunk)
-        nchunks = k_bulk + (spp - k_bulk * chunk + tail_chunk - 1) / tail_chunk;
+        if (fs > 0) {  // tail items cover [k_bulk * chunk, fin_first), final items [fin_first, spp)
+          const uint32_t n_tail = (spp - fs - k_bulk * chunk) / tail_chunk;
+          k_fin = k_bulk + n_tail;
+          fin_first = k_bulk * chunk + n_tail * tail_chunk;
+          nchunks = k_fin + (spp - fin_first + fin_chunk - 1) / fin_chunk;
+        } else {
+          nchunks = k_bulk + (spp - k_bulk * chunk + tail_chunk - 1) / tail_chunk;
+        }
         if (nchunks <= kMaxItemsPerPixel || chunk >= spp) break;
         chunk = std::min(spp, 2 * chunk);
         tail_chunk = std::min(chunk, 2 * tail_chunk);
+        fin_chunk = std::min(tail_chunk, 2 * fin_chunk);
       }
     }
     // Passes: the item partial sums of a call are 3 R per (pixel, chunk) -- C5 fp64 (3840 x 2160 at 4096 spp,
@@ -2197,6 +2191,7 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
       p.sc.spill_lanes = lanes;
     }
     if (prm->traversal == RT_TRAV_ORDERED) p.sc.has_flat = p.sc.has_wide = 0;
+    p.sc.cam64 = nullptr;  // set with the camera below (perspective only)
     p.O = (R4<R>*)sp;
     p.D = (R4<R>*)(sp + r4);
     p.T = (R4<R>*)(sp + 2 * r4);
@@ -2215,6 +2210,9 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     p.chunk = chunk;
     p.k_bulk = k_bulk;
     p.tail_chunk = tail_chunk;
+    p.k_fin = k_fin;
+    p.fin_chunk = fin_chunk;
+    p.fin_first = fin_first;
     p.spp = spp;
     p.first_sample = (uint32_t)std::max(0, prm->first_sample);
     p.W = (uint32_t)cam->image_width;
@@ -2229,6 +2227,7 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     }
     p.cam_mode = c->cam_host.mode;
     p.camx = (const CamDev*)c->camx.ptr;
+    if (p.cam_mode == RT_CAM_PERSPECTIVE) p.sc.cam64 = p.camx;
     p.seg_shards = (unsigned long long*)c->counters.ptr;
     const int K = prm->segments_per_launch > 0 ? std::min(prm->segments_per_launch, 64) : kAutoSegments;
     p.K = K;
@@ -2349,6 +2348,25 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
 extern "C" {
 
 int32_t rt_abi_version(void) { return RT_ABI_VERSION; }
+
+#define RT_STR2(x) #x
+#define RT_STR(x) RT_STR2(x)
+const char* rt_build_info(void) {
+  return "dev_only=" RT_STR(RT_DEV_ONLY) " wide_top_n=" RT_STR(RT_WIDE_TOP_N) " wide_top_stride=" RT_STR(
+      RT_WIDE_TOP_STRIDE) " wide_lds_stack=" RT_STR(RT_WIDE_LDS_STACK) " wide_waves_global=" RT_STR(RT_WIDE_WAVES_GLOBAL)
+#ifdef RT_SECTION_CLOCKS
+      " sections=1"
+#endif
+#ifdef RT_DEBUG_TRACE
+      " trace=1"
+#endif
+#ifdef RT_PRECISE_F32
+      " precise_f32=1"
+#endif
+      ;
+}
+#undef RT_STR
+#undef RT_STR2
 
 namespace {
 // g_sincos_tab (rt_device.h sincos2pi, fp64): (sin, cos)(2 pi j / 1024) in long double, rounded once,

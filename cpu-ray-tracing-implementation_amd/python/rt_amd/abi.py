@@ -88,6 +88,7 @@ class rt_scene_info(ctypes.Structure):
 # every symbol include/rt_hip.h declares, with its ctypes signature
 SIGNATURES = {
     "rt_abi_version": (c_int32, []),
+    "rt_build_info": (ctypes.c_char_p, []),
     "rt_context_create": (c_int32, [c_int32, ctypes.POINTER(ctypes.c_void_p)]),
     "rt_context_destroy": (None, [ctypes.c_void_p]),
     "rt_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
@@ -162,6 +163,11 @@ def load():
             raise RuntimeError(f"{path} has ABI {lib.rt_abi_version()}, this binding expects {ABI_VERSION}: rebuild")
         _lib = lib
     return _lib
+
+
+def build_info():
+    """The library's compile-time configuration (rt_build_info): {"dev_only": "0", "wide_top_n": "55", ...}."""
+    return dict(w.split("=", 1) for w in load().rt_build_info().decode().split())
 
 
 def scene_check(desc):

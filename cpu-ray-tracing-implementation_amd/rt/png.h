@@ -86,9 +86,10 @@ struct Huff {
   }
 };
 
-// `limit`: stop once this many bytes are out (the image's filtered size: a crafted stream cannot grow the
-// buffer past what the header's dimensions use; stb keeps decoding and ignores the surplus, so the pixels
-// are the same)
+// `limit`: keep at most this many bytes (the image's filtered size: a crafted stream cannot grow the buffer
+// past what the header's dimensions use). The rest of the stream is still decoded -- its codes, distances and
+// final block validated, its bytes counted and dropped -- as stb_image decodes the whole stream and then
+// ignores the surplus: a stream stb refuses (a bad code, no end of block, a truncated tail) is refused here too.
 inline bool inflate(const uint8_t* in, size_t n, std::vector<uint8_t>& out, std::string* err,
                     size_t limit = ~size_t(0)) {
   static const uint16_t lbase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
@@ -102,14 +103,18 @@ inline bool inflate(const uint8_t* in, size_t n, std::vector<uint8_t>& out, std:
     return false;
   };
   Bits b{in, n};
+  size_t total = out.size();  // bytes decoded, kept or not
+  auto put = [&](uint8_t v) {
+    if (out.size() < limit) out.push_back(v);
+    total++;
+  };
   for (;;) {
     const uint32_t last = b.get(1), type = b.get(2);
     if (type == 0) {  // stored
       b.align();
       const uint32_t len = b.get(16), nlen = b.get(16);
       if ((len ^ 0xFFFFu) != nlen) return fail("zlib: stored block length");
-      for (uint32_t i = 0; i < len; i++) out.push_back((uint8_t)b.get(8));
-      if (out.size() >= limit) return true;
+      for (uint32_t i = 0; i < len; i++) put((uint8_t)b.get(8));
     } else if (type == 1 || type == 2) {
       Huff lit, dist;
       uint8_t lens[320];
@@ -155,8 +160,7 @@ inline bool inflate(const uint8_t* in, size_t n, std::vector<uint8_t>& out, std:
         const int s = lit.decode(b);
         if (s < 0) return fail("zlib: bad literal/length code");
         if (s < 256) {
-          out.push_back((uint8_t)s);
-          if (out.size() >= limit) return true;
+          put((uint8_t)s);
         } else if (s == 256) {
           break;
         } else {
@@ -166,10 +170,14 @@ inline bool inflate(const uint8_t* in, size_t n, std::vector<uint8_t>& out, std:
           const int ds = dist.decode(b);
           if (ds < 0 || ds >= 30) return fail("zlib: bad distance code");
           const size_t d = dbase[ds] + b.get(dext[ds]);
-          if (d > out.size()) return fail("zlib: distance too far back");
-          const size_t from = out.size() - d;
-          for (size_t i = 0; i < len; i++) out.push_back(out[from + i]);
-          if (out.size() >= limit) return true;
+          if (d > total) return fail("zlib: distance too far back");
+          // (while bytes are kept, out holds every byte so far: from + i < out.size())
+          const size_t from = total - d;
+          for (size_t i = 0; i < len; i++) {
+            if (out.size() < limit)
+              out.push_back(out[from + i]);
+            total++;
+          }
         }
         if (b.bad) return fail("zlib: truncated");
       }

@@ -252,6 +252,12 @@ typedef struct rt_context rt_context;
 /* Library / ABI version, for the binding to check. */
 int32_t rt_abi_version(void);
 
+/* The build's compile-time configuration as "key=value" words (e.g. "dev_only=0 wide_top_n=55 ..."), so a
+ * harness can tell a development variant (scripts/build_variant.sh) from the product library: a build with
+ * dev_only != 0 instantiates one kernel family and answers RT_ERR_UNSUPPORTED for every other. No reference
+ * counterpart (the reference has no build variants). */
+const char* rt_build_info(void);
+
 /* Create a context on HIP device `device`. */
 rt_status rt_context_create(int32_t device, rt_context** out);
 void rt_context_destroy(rt_context* ctx);

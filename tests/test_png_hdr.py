@@ -98,3 +98,27 @@ def test_oversized_headers_are_refused_before_allocating(dump, tmp_path):
     ok.write_bytes(_png(3, 2, 2, 8, zlib.compress(b"\0" + bytes(range(9)) + b"\0" + bytes(range(9, 18)))))
     w, h, tex = dump(str(ok))
     assert (w, h) == (3, 2) and len(tex) == 18
+
+
+def test_a_corrupt_stream_tail_past_the_pixels_is_refused(dump, tmp_path):
+    # The pixels need the stream's first 18 filtered bytes; the stream goes on and is cut off before its final
+    # block ends. stb_image inflates the whole stream and refuses it; so does our inflate, which keeps only the
+    # bytes the image needs but decodes the rest to the end (round-5 advisor: it used to stop at the image's
+    # size and accept such a file).
+    import random
+    import zlib
+    raw = b"\0" + bytes(range(9)) + b"\0" + bytes(range(9, 18))
+    rnd = random.Random(7)
+    surplus = bytes(rnd.randrange(256) for _ in range(3000))
+    whole = zlib.compress(raw + surplus, 9)
+    cases = {"tail_ok.png": (whole, True), "tail_cut.png": (whole[:len(whole) // 2], False),
+             "tail_stored_cut.png": (zlib.compress(raw + surplus, 0)[:200], False)}
+    stb = os.path.join(REPO, "oracle", "_ref", "stb_decode")
+    for name, (idat, decodes) in cases.items():
+        p = tmp_path / name
+        p.write_bytes(_png(3, 2, 2, 8, idat))
+        w, h, tex = dump(str(p))
+        assert ((w, h) == (3, 2) and len(tex) == 18) if decodes else ((w, h) == (0, 0) and tex == b""), name
+        if os.path.exists(stb):  # the reference's decoder agrees (oracle/_ref is built where /root/reference is)
+            out = subprocess.run([stb, str(p)], capture_output=True, text=True).stdout.split("\n")
+            assert (out[0] == "3 2") == decodes, (name, out[:2])
