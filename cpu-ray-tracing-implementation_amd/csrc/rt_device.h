@@ -2055,21 +2055,30 @@ __device__ __forceinline__ V<R> onb_transform(const Onb<R>& b, V<R> v) {  // onb
   return r;
 }
 // random_in_unit_sphere (utility.h:30-42): a point ON the unit sphere
+// (the _sc forms take sin/cos(2 pi u) computed by the caller: shade's NL form computes one for every lane)
 template <class R>
-__device__ __forceinline__ V<R> on_sphere(R u1, R u2) {
+__device__ __forceinline__ V<R> on_sphere_sc(R u1, R sp, R cp) {
   R cos_theta = R(1) - R(2) * u1;
   R sin_theta = fsqrt01(R(1) - cos_theta * cos_theta);
-  R sp, cp;
-  sincos2pi(u2, sp, cp);
   return mkv(sin_theta * cp, cos_theta, sin_theta * sp);
 }
+template <class R>
+__device__ __forceinline__ V<R> on_sphere(R u1, R u2) {
+  R sp, cp;
+  sincos2pi(u2, sp, cp);
+  return on_sphere_sc(u1, sp, cp);
+}
 // random_cosine_direction (utility.h:61-69)
+template <class R>
+__device__ __forceinline__ V<R> cosine_dir_sc(R r2, R sp, R cp) {
+  R sr2 = fsqrt01(r2);
+  return mkv(cp * sr2, fsqrt01(R(1) - r2), sp * sr2);
+}
 template <class R>
 __device__ __forceinline__ V<R> cosine_dir(R r1, R r2) {
   R sp, cp;
   sincos2pi(r1, sp, cp);
-  R sr2 = fsqrt01(r2);
-  return mkv(cp * sr2, fsqrt01(R(1) - r2), sp * sr2);
+  return cosine_dir_sc(r2, sp, cp);
 }
 
 // hittable_pdf over the light (hittable_list.h:39-50 -> quad.h:66-78 / sphere.h:76-81 / hittable.h:39-41)

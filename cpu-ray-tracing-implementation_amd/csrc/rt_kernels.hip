@@ -119,8 +119,6 @@ constexpr uint32_t kItemsTarget = 4000000;
 // item partial sums of one pass at most (render(): a call needing more renders its chunks in passes)
 constexpr uint64_t kPartialBudget = 2ull << 30;
 constexpr uint32_t kMinAutoChunk = 2;
-constexpr double kItemFinalFrac = 0.0;  // (auto_final_frac)
-constexpr uint32_t kItemFinalChunk = 2;
 static uint32_t auto_chunk(bool flat) {
   return std::max(1u, flat ? env_u32("RT_ITEM_CHUNK_FLAT", 2 * kAutoChunk) : env_u32("RT_ITEM_CHUNK", kAutoChunk / 2));
 }
@@ -130,9 +128,6 @@ static uint32_t auto_tail_chunk(bool flat) {
 static double auto_tail_frac(bool flat) {
   return std::min(1.0, std::max(0.0, flat ? env_f64("RT_ITEM_TAIL_FRAC_FLAT", 0.125) : env_f64("RT_ITEM_TAIL_FRAC", 0.5)));
 }
-// the final tier of the layout: the last final_frac of every pixel's samples in items of final_chunk (render())
-static double auto_final_frac() { return std::min(1.0, std::max(0.0, env_f64("RT_ITEM_FINAL_FRAC", kItemFinalFrac))); }
-static uint32_t auto_final_chunk() { return std::max(1u, env_u32("RT_ITEM_FINAL_CHUNK", kItemFinalChunk)); }
 constexpr int kAutoSegments = 16;  // segments each slot advances per k_step launch
 // persistent schedule: upper bound of the grid's lanes. The dynamic schedule (persist 2) cuts the
 // grid to what the chip holds resident; the static one (persist 1) launches them all (~10x the
@@ -147,8 +142,6 @@ constexpr uint32_t kHeads = 8;
 constexpr uint32_t kHeadStride = 64;  // 256 B apart: one L2 line per head
 constexpr uint32_t kQBatch = 64;
 constexpr uint32_t kNoItem = 0xFFFFFFFFu;
-constexpr double kQueueTailLanes = 0.0;  // (launch_one)
-constexpr uint32_t kQueueTailBatch = 8;
 
 template <class R>
 struct alignas(4 * sizeof(R)) R4 {
@@ -182,10 +175,9 @@ struct Params {
   const uint32_t* queue;   // live slots, or null = slots [0, n)
   uint32_t n;
   uint32_t P, npix, n_items, chunk, spp, first_sample, W;
-  // up to three item sizes: chunks [0, k_bulk) hold `chunk` samples, the later ones (the frame's last
-  // items in dequeue order) `tail_chunk` <= chunk samples each, and from chunk k_fin on (the final tier;
-  // 0xFFFFFFFF: none) `fin_chunk` samples from sample fin_first on
-  uint32_t k_bulk, tail_chunk, k_fin, fin_chunk, fin_first;
+  // two item sizes: chunks [0, k_bulk) hold `chunk` samples, the later ones (the frame's last
+  // items in dequeue order) `tail_chunk` <= chunk samples each
+  uint32_t k_bulk, tail_chunk;
   // the render's chunks come in passes (render(): the partial sums of one pass fit a memory budget): this
   // launch's items are chunks [chunk0, chunk0 + n_items / npix) of every pixel
   uint32_t chunk0;
@@ -203,9 +195,6 @@ struct Params {
   // the grid is what the chip holds resident and lanes pull items from the per-XCD heads
   int32_t persist;
   uint32_t* heads;  // kHeads dequeue counters, kHeadStride words apart (persist 2)
-  // persist 2: items [0, q_split) are handed out in batches of kQBatch, the frame's last items [q_split,
-  // n_items) in batches of q_tbatch (launch_one; q_split is a multiple of kHeads * kQBatch)
-  uint32_t q_split, q_tbatch;
   uint64_t seg_cap;  // a lane never needs more segments than this (its items * chunk * max_depth)
   uint32_t* fault;   // set when a lane hits seg_cap (internal error, reported by the host)
 };
@@ -359,21 +348,21 @@ __device__ __forceinline__ uint32_t* wave_queue() {
   return wq + 2 * (threadIdx.x >> 6);
 }
 
-// A batch of items for the calling lane's wave: the block's own head first (blocks b and b + 8 share an
-// XCD, so a head's counter stays in one XCD's traffic), then the others. Ticket j of head h is batch j *
-// kHeads + h of kQBatch items while j < q_split / (kHeads * kQBatch); the tickets after those are batches of
-// q_tbatch items over [q_split, n_items), numbered the same way. Returns the first item, or kNoItem once
-// every head has run past the item space.
-template <class R>
-__device__ __forceinline__ uint32_t grab_batch(const Params<R>& p) {
+// A batch of kQBatch items for the calling lane's wave: the block's own head first (blocks b and
+// b + 8 share an XCD, so a head's counter stays in one XCD's traffic), then the others. Returns the
+// first item, or kNoItem once every head has run past the item space.
+// (Round 6 measured two ways of shortening the frame's end at one rank of eight, C2 fp64: the last 1-4 x the
+// grid's lanes of items handed out in batches of 8 instead of 64 -- 0.856 / 0.855 / 0.854 / 0.856 of linear
+// at 8 emulated ranks for 0 / 1 / 2 / 4 x; batches of 1, 0.699 -- and a third item tier, the last 1/64 - 1/16 of
+// every pixel's samples in items of 1-4, 0.858 - 0.868 against 0.860 - 0.862, within the spread, and +8 B of
+// spill in the C5 fp32 kernel (r06a, r06b; profiles/r06b_ab_summary.txt). Neither is kept.)
+__device__ __forceinline__ uint32_t grab_batch(uint32_t* heads, uint32_t n_items) {
   const uint32_t g = blockIdx.x & (kHeads - 1);
-  const uint32_t ja = p.q_split / (kHeads * kQBatch);
   for (uint32_t t = 0; t < kHeads; t++) {
     const uint32_t h = (g + t) & (kHeads - 1);
-    const uint32_t j = atomicAdd(p.heads + h * kHeadStride, 1u);
-    const uint64_t first = j < ja ? ((uint64_t)j * kHeads + h) * kQBatch
-                                  : p.q_split + ((uint64_t)(j - ja) * kHeads + h) * p.q_tbatch;
-    if (first < p.n_items) return (uint32_t)first;
+    const uint32_t j = atomicAdd(heads + h * kHeadStride, 1u);
+    const uint64_t first = ((uint64_t)j * kHeads + h) * kQBatch;
+    if (first < n_items) return (uint32_t)first;
   }
   return kNoItem;
 }
@@ -401,14 +390,14 @@ __device__ __forceinline__ uint32_t next_item_dyn(const Params<R>& p) {
     off += take;
     if (off >= k || qe == kNoItem) break;  // served, or the wave already found every head dry
     uint32_t b = kNoItem;
-    if (lane == leader) b = grab_batch(p);
+    if (lane == leader) b = grab_batch(p.heads, p.n_items);
     b = __shfl(b, (int)leader);
     if (b == kNoItem) {  // remember it: a dry scan stalls the wave for kHeads atomics
       qn = qe = kNoItem;
       break;
     }
     qn = b;
-    qe = min(b + (b < p.q_split ? kQBatch : p.q_tbatch), p.n_items);
+    qe = min(b + kQBatch, p.n_items);
   }
   if (lane == leader) {
     __hip_atomic_store(wq, qn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
@@ -427,10 +416,9 @@ __device__ __forceinline__ void item_range(const Params<R>& p, uint32_t item, ui
   const uint32_t chunk = lchunk + p.chunk0;
   // fp64 items are uniform (the host never gives them a tail): compiled out, the select costs
   // the fp64 Cornell kernel 10 VGPRs, 3 -> 2 waves per SIMD (C2 f64 5.22 -> 4.08 Gsamples/s)
-  const bool bulk = chunk < p.k_bulk, fin = chunk >= p.k_fin;
-  first = bulk ? chunk * p.chunk
-               : (fin ? p.fin_first + (chunk - p.k_fin) * p.fin_chunk : p.k_bulk * p.chunk + (chunk - p.k_bulk) * p.tail_chunk);
-  end = min(first + (bulk ? p.chunk : (fin ? p.fin_chunk : p.tail_chunk)), p.spp);
+  const bool bulk = chunk < p.k_bulk;
+  first = bulk ? chunk * p.chunk : p.k_bulk * p.chunk + (chunk - p.k_bulk) * p.tail_chunk;
+  end = min(first + (bulk ? p.chunk : p.tail_chunk), p.spp);
 }
 // the pixel's RNG key and the end of the item's samples: kept, or (LEAN) recomputed
 template <class R, class PS>
@@ -770,11 +758,26 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
       const uint32_t bounce = (uint32_t)s.bounce;
       uint32_t js = 0;
       auto U = [&]() { return to_unit<R>(draw_u32(s.ks, dim_scatter(bounce, js++))); };
+      // NL (lambertian / metal / dielectric, no light): the scatter draws are pure functions of (path key,
+      // dimension), and lambertian's cosine sample and metal's fuzz sample each need sin/cos(2 pi u) of one of the
+      // first two draws -- so both draws and one sincos are computed by every lane before the material branches,
+      // which then hold no trigonometry (the same operations on the same values: bit-identical)
+      [[maybe_unused]] R nl_u1 = R(0), nl_u2 = R(0), nl_sp = R(0), nl_cp = R(0);
+      constexpr bool kNlTrig = NL;  // C3 fp32 48.16 -> 47.60 ms/frame, fp64 64.70 -> 64.09 (r06b)
+      if constexpr (kNlTrig) {
+        nl_u1 = to_unit<R>(draw_u32(s.ks, dim_scatter(bounce, 0)));
+        nl_u2 = to_unit<R>(draw_u32(s.ks, dim_scatter(bounce, 1)));
+        sincos2pi(m.kind == M_METAL ? nl_u2 : nl_u1, nl_sp, nl_cp);  // on_sphere: phi = 2 pi u2; cosine: 2 pi u1
+      }
       if (!LL && m.kind == M_METAL) {  // material.h:85-92
         V<R> dir = unit(reflect(d, n));
-        R u1 = U();
-        R u2 = U();
-        new_d = dir + m.fuzz * unit(on_sphere(u1, u2));
+        if constexpr (kNlTrig) {
+          new_d = dir + m.fuzz * unit(on_sphere_sc(nl_u1, nl_sp, nl_cp));
+        } else {
+          R u1 = U();
+          R u2 = U();
+          new_d = dir + m.fuzz * unit(on_sphere(u1, u2));
+        }
         s.thr = s.thr * att;
       } else if (!LL && m.kind == M_DIELECTRIC) {  // material.h:113-131
         R ri = front ? fdiv(R(1), m.refr) : m.refr;
@@ -784,7 +787,7 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
         bool cant = ri * sin_t > R(1);
         R r0 = fdiv(R(1) - ri, R(1) + ri);
         r0 = r0 * r0;
-        if (cant || (r0 + (R(1) - r0) * pow5(R(1) - cos_t)) > U())
+        if (cant || (r0 + (R(1) - r0) * pow5(R(1) - cos_t)) > (kNlTrig ? nl_u1 : U()))
           new_d = reflect(ud, n);
         else
           new_d = refract(ud, n, ri);
@@ -834,9 +837,13 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
         // the pdf against the unit one, and the ratio |n| is the reference's (quirk kept)
         bool own_pdf = false;
         if (NL || (!LL && ld_here(&Lt->kind) == L_NONE)) {
-          R u1 = U();
-          R u2 = U();
-          dir = iso ? unit(on_sphere(u1, u2)) : cos_dir(u1, u2);
+          if constexpr (kNlTrig) {  // NL has no isotropic material
+            dir = onb_transform(b, cosine_dir_sc(nl_u2, nl_sp, nl_cp));
+          } else {
+            R u1 = U();
+            R u2 = U();
+            dir = iso ? unit(on_sphere(u1, u2)) : cos_dir(u1, u2);
+          }
           own_pdf = iso || unit_n;
           if (!own_pdf) pv = fmax(R(0), div_pi(cos_n(unit(dir))));
         } else {  // dual_pdf(hittable_pdf(light), material pdf) (camera.h:227-239, pdf.h:48-61)
@@ -1817,10 +1824,6 @@ uint32_t resident_blocks(const void* kern, int dev, size_t lds) {
   return r;
 }
 
-// The dynamic schedule's tail (launch_one): the last RT_QTAIL_LANES x (grid lanes) items of a launch are handed
-// out in batches of RT_QTAIL_BATCH items instead of kQBatch
-static double queue_tail_lanes() { return std::max(0.0, env_f64("RT_QTAIL_LANES", kQueueTailLanes)); }
-static uint32_t queue_tail_batch() { return env_u32("RT_QTAIL_BATCH", kQueueTailBatch); }
 // lanes of the last persistent launch on this host thread (rt_counters.grid_lanes)
 thread_local uint64_t t_grid_lanes = 0;
 
@@ -1832,11 +1835,6 @@ void launch_one(KernelT kern, Params<R> p, uint32_t grid, hipStream_t st, size_t
     if (res > 0) grid = std::min<uint32_t>(grid, res);
     p.P = grid * kBlock;
     p.seg_cap = (uint64_t)p.n_items * p.chunk * (uint64_t)p.max_depth + 1;
-    // the frame's last items in small batches, so that a wave does not hold a batch of them queued while
-    // lanes of other waves run dry (the tail of a short frame: one rank of eight)
-    const uint64_t tail = std::min<uint64_t>(p.n_items, (uint64_t)(queue_tail_lanes() * p.P));
-    p.q_split = (uint32_t)((p.n_items - tail) / (kHeads * kQBatch) * (kHeads * kQBatch));
-    p.q_tbatch = p.q_split < p.n_items ? std::max<uint32_t>(1u, std::min(kQBatch, queue_tail_batch())) : kQBatch;
   } else if (p.persist) {  // the lanes stride over the items by the grid's lane count
     p.P = grid * kBlock;
     p.seg_cap = ((uint64_t)p.n_items + p.P - 1) / p.P * p.chunk * (uint64_t)p.max_depth + 1;
@@ -2103,27 +2101,15 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     // items of tail_chunk samples; both depend on spp alone, so the image is the same for any
     // tiling or rank count.
     uint32_t chunk = chunk0, tail_chunk = chunk0, k_bulk = (spp + chunk0 - 1) / chunk0, nchunks = k_bulk;
-    uint32_t k_fin = 0xFFFFFFFFu, fin_chunk = chunk0, fin_first = spp;
     if (prm->samples_per_item <= 0) {  // (fp64 too since round 3: round 2 kept uniform items of 16 for it)
       const uint32_t ts = std::min<uint32_t>(spp, (uint32_t)((double)spp * auto_tail_frac(flat_prog) + 0.5));
-      // the final tier (RT_ITEM_FINAL_FRAC > 0): the last fs samples of the tail in items of fin_chunk
-      const uint32_t fs = std::min<uint32_t>(ts, (uint32_t)((double)spp * auto_final_frac() + 0.5));
       tail_chunk = std::min(chunk, auto_tail_chunk(flat_prog));
-      fin_chunk = std::min(tail_chunk, auto_final_chunk());
       for (;;) {
         k_bulk = (spp - ts) / chunk;  // bulk items cover [0, k_bulk * chunk)
-        if (fs > 0) {  // tail items cover [k_bulk * chunk, fin_first), final items [fin_first, spp)
-          const uint32_t n_tail = (spp - fs - k_bulk * chunk) / tail_chunk;
-          k_fin = k_bulk + n_tail;
-          fin_first = k_bulk * chunk + n_tail * tail_chunk;
-          nchunks = k_fin + (spp - fin_first + fin_chunk - 1) / fin_chunk;
-        } else {
-          nchunks = k_bulk + (spp - k_bulk * chunk + tail_chunk - 1) / tail_chunk;
-        }
+        nchunks = k_bulk + (spp - k_bulk * chunk + tail_chunk - 1) / tail_chunk;
         if (nchunks <= kMaxItemsPerPixel || chunk >= spp) break;
         chunk = std::min(spp, 2 * chunk);
         tail_chunk = std::min(chunk, 2 * tail_chunk);
-        fin_chunk = std::min(tail_chunk, 2 * fin_chunk);
       }
     }
     // Passes: the item partial sums of a call are 3 R per (pixel, chunk) -- C5 fp64 (3840 x 2160 at 4096 spp,
@@ -2210,9 +2196,6 @@ rt_status render(rt_context* c, const rt_camera_desc* cam, const rt_render_param
     p.chunk = chunk;
     p.k_bulk = k_bulk;
     p.tail_chunk = tail_chunk;
-    p.k_fin = k_fin;
-    p.fin_chunk = fin_chunk;
-    p.fin_first = fin_first;
     p.spp = spp;
     p.first_sample = (uint32_t)std::max(0, prm->first_sample);
     p.W = (uint32_t)cam->image_width;
