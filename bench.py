@@ -674,8 +674,10 @@ def main():
                                                 alt_name == "f64")
             if cpu:
                 alt_line["parity"] = parity_tiles(fba, W, ptiles, ref_px, rel_tol=1e-9 if alt_name == "f64" else None)
-                alt_line["speedup_vs_cpu_baseline"] = round(va / cpu["value"], 1)
-                alt_line["speedup_per_segment"] = round(va * sa / (cpu["value"] * cpu["segments_per_sample"]), 1)
+                tree = "baseline_tree" in cpu  # (C4: see the headline object's ratio_vs_reference_tree)
+                alt_line["ratio_vs_reference_tree" if tree else "speedup_vs_cpu_baseline"] = round(va / cpu["value"], 1)
+                alt_line["ratio_vs_reference_tree_per_segment" if tree else "speedup_per_segment"] = round(
+                    va * sa / (cpu["value"] * cpu["segments_per_sample"]), 1)
         lit = None
         if cpu and scene_name == "sponza" and not args.no_lit_parity:
             lit = lit_parity(ctx, width, aspect, spp, depth, args.seed, threads,
@@ -710,8 +712,12 @@ def main():
             # it traces more segments per sample
             line["speedup_per_segment"] = round(value * seg_per_sample / (cpu["value"] * cpu["segments_per_sample"]),
                                                 1)
-            if "baseline_tree" in cpu:  # the ratio compares trees as much as hardware: say which
-                line["speedup_baseline_tree"] = "x-median (bvh_node.h:13-47)"
+            if "baseline_tree" in cpu:
+                # the CPU baseline runs the reference's own x-median tree over 262k triangles (bvh_node.h:13-47), the
+                # GPU a SAH tree: the ratio compares trees as much as hardware, so it is not reported as a speedup
+                line["ratio_vs_reference_tree"] = line.pop("speedup_vs_cpu_baseline")
+                line["ratio_vs_reference_tree_per_segment"] = line.pop("speedup_per_segment")
+                line["speedup_baseline_tree"] = "x-median (bvh_node.h:13-47): not a like-for-like speedup"
         print(json.dumps(line), flush=True)
     ctx.close()
     if world > 1:

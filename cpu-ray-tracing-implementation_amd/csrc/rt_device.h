@@ -424,8 +424,8 @@ struct DevScene {
 #ifndef RT_WIDE_LDS_STACK
 #define RT_WIDE_LDS_STACK 12
 #endif
-#ifndef RT_WIDE_LDS_STACK_F64
-#define RT_WIDE_LDS_STACK_F64 24
+#ifndef RT_WIDE_LDS_STACK_F64  // 18 since round 6: the fp64 LL kernel's LDS also holds the throughput (Path LT)
+#define RT_WIDE_LDS_STACK_F64 18
 #endif
 // stack entries per lane kept in LDS for a tree in HBM, by ray precision (fp32: fewer, so the LDS also holds
 // the top of the tree and 8 blocks fit a CU; C4 fp32, stack / top nodes / waves: 24 / 0 / 6 309.4 ms/frame,
@@ -594,6 +594,9 @@ __device__ __forceinline__ bool tri_test(V<R> p0, V<R> e1, V<R> e2, V<R> o, V<R>
     b1 = fdiv(dot(s2, d), den);
   }
   if (th < tmin || th > tmax) return false;
+  // (round 6 measured an fp32 edge tolerance of 8 u |s| |e| |d| / |det| -- the tests' rounding bound -- against the
+  // fp32 misses of triangles the fp64 test hits, e.g. a grazing ray through one of the C4 stand-in's grids (r06d
+  // traces): C4 lit fp32 against fp64 over 400 tiles went from 1.71e-4 to 1.3e-3, every triangle growing by it)
   if (b0 < R(0) || b1 < R(0) || b0 + b1 > R(1)) return false;
   if (th != th) return false;  // 0/0 determinant: the reference's comparisons reject NaN too
   t = th;

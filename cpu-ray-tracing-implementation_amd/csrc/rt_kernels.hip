@@ -50,6 +50,15 @@ constexpr int kBlock = 256;
 // background
 // RT_BG_SOLID_FAST (retired in round 6, always on): shade: nor against another solid background when |d| < 500 (the
 // test always hits)
+#ifndef RT_LLI_SHARED_TRIG  // shade LLI: one sincos for the isotropic and lambertian lanes of a material sample
+#define RT_LLI_SHARED_TRIG 1
+#endif
+#ifndef RT_WIDE_THR_LDS_F64  // the fp64 LL kernel over a tree in HBM keeps the path throughput in LDS (Path LT)
+#define RT_WIDE_THR_LDS_F64 1
+#endif
+#ifndef RT_LLI_THR_LDS  // the fp32 LLI volume kernel keeps the path throughput in LDS (Path LT)
+#define RT_LLI_THR_LDS 1
+#endif
 #ifndef RT_LINEAR_WAVES
 #define RT_LINEAR_WAVES 6
 #endif
@@ -210,6 +219,12 @@ __device__ __forceinline__ double* cold_doubles() {
   __shared__ double w[kColdDoubles * kBlock];
   return w + threadIdx.x;
 }
+// the throughput of an LT path ([component][lane])
+template <class R>
+__device__ __forceinline__ R* cold_thr() {
+  __shared__ R w[3 * kBlock];
+  return w + threadIdx.x;
+}
 // the fp64 item sum of an LC path ([component][lane]; fp32 keeps it in three of the cold words)
 __device__ __forceinline__ __attribute__((unused)) double* cold_acc64() {
   __shared__ double w[3 * kBlock];
@@ -225,11 +240,13 @@ __device__ __forceinline__ __attribute__((unused)) double* cold_acc64() {
 // traversal state competes with them (the wide BVH kernels), at a few integer and fp64 operations per
 // sample.
 // NORAD: no radiance register either (shade adds emission straight into the item's running sum).
-template <class R, bool LC = false, bool LEAN = false, bool NORAD = LEAN>
+// LT: the throughput in the lane's LDS words too (cold_thr; the fp32 LLI volume kernel, whose 72-VGPR budget
+// otherwise spills it to scratch every segment)
+template <class R, bool LC = false, bool LEAN = false, bool NORAD = LEAN, bool LT = false>
 struct Path {
   static constexpr bool kLean = LEAN;
   static constexpr bool kNoRad = NORAD;
-  V<R> o, d, thr, rad;
+  V<R> o, d, thr_, rad;
   R tm;
   int32_t bounce;
   uint32_t ks;
@@ -243,6 +260,19 @@ struct Path {
   uint64_t t0_;  // development: wall clock at the item's start
 #endif
   enum { kAcc = 0, kKa = 3, kItem, kSample, kSend, kXy };
+  __device__ __forceinline__ V<R> thr() const {
+    if constexpr (LT) return mkv(cold_thr<R>()[0], cold_thr<R>()[kBlock], cold_thr<R>()[2 * kBlock]);
+    else return thr_;
+  }
+  __device__ __forceinline__ void set_thr(V<R> v) {
+    if constexpr (LT) {
+      cold_thr<R>()[0] = v.x;
+      cold_thr<R>()[kBlock] = v.y;
+      cold_thr<R>()[2 * kBlock] = v.z;
+    } else {
+      thr_ = v;
+    }
+  }
   __device__ __forceinline__ static uint32_t& w(int k) { return cold_words()[k * kBlock]; }
   __device__ __forceinline__ V<R> acc() const {
     if constexpr (LC && sizeof(R) == 8) {
@@ -315,7 +345,7 @@ __device__ __forceinline__ void load_path(const Params<R>& p, uint32_t slot, R4<
   s.tm = Ov.w;
   s.d = mkv(Dv.x, Dv.y, Dv.z);
   s.bounce = (int32_t)Dv.w;
-  s.thr = mkv(Tv.x, Tv.y, Tv.z);
+  s.set_thr(mkv(Tv.x, Tv.y, Tv.z));
   s.rad = mkv(Lv.x, Lv.y, Lv.z);
   s.set_acc(mkv(Av.x, Av.y, Av.z));
   s.set_ka(S.x);
@@ -334,7 +364,8 @@ __device__ __forceinline__ void store_path(const Params<R>& p, uint32_t slot, co
   p.D[slot] = {s.d.x, s.d.y, s.d.z, R(s.bounce)};
   if (s.bounce < 0) return;
   p.O[slot] = {s.o.x, s.o.y, s.o.z, s.tm};
-  p.T[slot] = {s.thr.x, s.thr.y, s.thr.z, R(0)};
+  const V<R> thr = s.thr();
+  p.T[slot] = {thr.x, thr.y, thr.z, R(0)};
   p.L[slot] = {s.rad.x, s.rad.y, s.rad.z, R(0)};
   const V<R> acc = s.acc();
   p.A[slot] = {acc.x, acc.y, acc.z, R(0)};
@@ -535,7 +566,7 @@ __device__ __forceinline__ void begin_sample(const Params<R>& p, PS& s) {
   s.d = mkv(R(d.x), R(d.y), R(d.z));
   s.tm = R(tm);
   s.bounce = 0;
-  s.thr = mkv(R(1), R(1), R(1));
+  s.set_thr(mkv(R(1), R(1), R(1)));
   if constexpr (!PS::kNoRad) s.rad = mkv(R(0), R(0), R(0));
   s.xe = kNoHit;
   s.xi = -1;
@@ -607,14 +638,14 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
     const bool bg_solid = bgt != nullptr && !bg_black && ld_here(&bgt->kind) == T_SOLID &&
                           dd2 < R(250000) && dd2 > R(0);
     if (bg_solid) {
-      add = s.thr * mkv(ld_here(&bgt->c0[0]), ld_here(&bgt->c0[1]), ld_here(&bgt->c0[2]));
+      add = s.thr() * mkv(ld_here(&bgt->c0[0]), ld_here(&bgt->c0[1]), ld_here(&bgt->c0[2]));
       has_add = true;
     } else if (sc.background >= 0 && !bg_black) {
       R tb;
       if (sphere_roots<R>(o.x, o.y, o.z, d.x, d.y, d.z, o.x, o.y, o.z, R(1), R(0.001), Num<R>::inf(), false, tb)) {
         double bu = 0, bv = 0;
         if constexpr (CAMX) sphere_uv(tb * d, bu, bv);  // the unit sphere about the origin (camera.h:184-187)
-        add = s.thr * tex_sample<R, CAMX>(sc, sc.texs[sc.background], o + tb * d, bu, bv);
+        add = s.thr() * tex_sample<R, CAMX>(sc, sc.texs[sc.background], o + tb * d, bu, bv);
         has_add = true;
       }
     }
@@ -749,7 +780,7 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
     }
     if (is_light) {  // material.h:211-215; no scatter
       if (front) {
-        add = s.thr * (LL ? col : tex_sample<R, CAMX>(sc, m.tx, pw, hu, hv));
+        add = s.thr() * (LL ? col : tex_sample<R, CAMX>(sc, m.tx, pw, hu, hv));
         has_add = true;
       }
       done = true;
@@ -778,7 +809,7 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
           R u2 = U();
           new_d = dir + m.fuzz * unit(on_sphere(u1, u2));
         }
-        s.thr = s.thr * att;
+        s.set_thr(s.thr() * att);
       } else if (!LL && m.kind == M_DIELECTRIC) {  // material.h:113-131
         R ri = front ? fdiv(R(1), m.refr) : m.refr;
         V<R> ud = unit(d);
@@ -791,7 +822,7 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
           new_d = reflect(ud, n);
         else
           new_d = refract(ud, n, ri);
-        s.thr = s.thr * att;
+        s.set_thr(s.thr() * att);
       } else if (!LL && !NL && m.kind == M_GLOSS && to_unit<R>(draw_u32(s.ks, dim_scatter(bounce, js))) <= m.spec) {
         // gloss, specular branch (material.h:158-167): kDetermined, attenuation 1,
         // direction unit(lerp(smoothness, cosine-hemisphere sample about n, reflect(d_in, n)))
@@ -857,6 +888,11 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
             dir = from_light ? dl : dc;
           } else if (from_light) {
             dir = light_random(Lt, pw, u1, u2);
+          } else if constexpr (LLI && RT_LLI_SHARED_TRIG) {
+            // the isotropic (on_sphere: phi = 2 pi u2) and lambertian (cosine: phi = 2 pi u1) lanes share one sincos
+            R sp, cp;
+            sincos2pi(iso ? u2 : u1, sp, cp);
+            dir = iso ? unit(on_sphere_sc(u1, sp, cp)) : onb_transform(b, cosine_dir_sc(u2, sp, cp));
           } else {
             dir = iso ? unit(on_sphere(u1, u2)) : cos_dir(u1, u2);
           }
@@ -864,7 +900,7 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
           pv = R(0.5) * light_pdf<R, kMixSel>(Lt, pw, dir, from_light) + R(0.5) * mp;
         }
         if (own_pdf) {
-          s.thr = s.thr * att;
+          s.set_thr(s.thr() * att);
         } else {
           R ps;
           if (iso) {
@@ -874,15 +910,18 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
             ps = c < R(0) ? R(0) : div_pi(c);
           }
           if constexpr (sizeof(R) == 8)
-            s.thr = s.thr * ((att * ps) / pv);  // camera.h:238 grouping on the parity path
+            s.set_thr(s.thr() * ((att * ps) / pv));  // camera.h:238 grouping on the parity path
           else  // a zero mixture pdf (the reference's 0/0 = NaN) ends the path
-            s.thr = pv > R(0) ? s.thr * (att * fdiv(ps, pv)) : mkv(R(0), R(0), R(0));
+            s.set_thr(pv > R(0) ? s.thr() * (att * fdiv(ps, pv)) : mkv(R(0), R(0), R(0)));
         }
         new_d = dir;
       }
       new_o = pw;
       if (s.bounce + 1 >= p.max_depth) done = true;  // ray_color(.., 0) returns 0 (camera.h:194)
-      if (s.thr.x == R(0) && s.thr.y == R(0) && s.thr.z == R(0)) done = true;
+      {
+        const V<R> thr = s.thr();
+        if (thr.x == R(0) && thr.y == R(0) && thr.z == R(0)) done = true;
+      }
     }
   }
   if (has_add) {
@@ -956,6 +995,7 @@ struct LinearTrav {
   static constexpr bool kLean = false;  // (LLI lean: 7 waves 1,094 -> 1,117 ms/frame; 8 waves 48 B spilled, r06a)
   static constexpr bool kNoRad = VOL;
   static constexpr bool kColdLds = VOL;
+  static constexpr bool kThrLds = RT_LLI_THR_LDS && VOL && LLI && sizeof(R) == 4;  // (Path LT)
   template <class PS>
   __device__ __forceinline__ static void run(const DevScene<R>& sc, const Node<R>*, const PS& s, Keys k,
                                              uint32_t*, R& t, uint32_t& e, int32_t& i, uint32_t&) {
@@ -993,6 +1033,7 @@ struct FlatTrav {
   static constexpr bool kLean = false;
   static constexpr bool kNoRad = true;  // 6 VGPRs in fp64 (its item sum is in LDS)
   static constexpr bool kColdLds = sizeof(R) == 8;
+  static constexpr bool kThrLds = false;
   template <class PS>
   __device__ __forceinline__ static void run(const DevScene<R>& sc, const Node<R>*, const PS& s, Keys, uint32_t*,
                                              R& t, uint32_t& e, int32_t& i, uint32_t& nm) {
@@ -1047,6 +1088,7 @@ struct StackTrav {
   static constexpr bool kLean = false;
   static constexpr bool kNoRad = false;
   static constexpr bool kColdLds = false;  // its LDS holds the traversal stacks
+  static constexpr bool kThrLds = false;
   template <class PS>
   __device__ __forceinline__ static void run(const DevScene<R>& sc, const Node<R>* nodes, const PS& s, Keys k,
                                              uint32_t* stk, R& t, uint32_t& e, int32_t& i, uint32_t&) {
@@ -1107,6 +1149,10 @@ struct WideTrav {
   static constexpr bool kFlat = false;
   static constexpr bool kWide = true;
   static constexpr bool kColdLds = false;  // its LDS holds the tree and the stacks
+  // (Path LT) the fp64 LL kernel over a tree in HBM (C4): its throughput in LDS, 6 KB a block, for which its LDS stack
+  // keeps 18 entries instead of 24: 339.2 -> 331.8 ms/frame, writes 16.4 -> 9.4 GB per launch (r06d). The fp64 NL
+  // kernel over an LDS tree (C3) lost with it: 63.55 -> 68.08 ms/frame
+  static constexpr bool kThrLds = RT_WIDE_THR_LDS_F64 && sizeof(R) == 8 && !LDSN && LL;
   static constexpr bool kTablesLds = false;
   static constexpr bool kLean = true;  // registers for the traversal (fewer spills)
   static constexpr bool kNoRad = true;
@@ -1323,7 +1369,7 @@ __device__ __forceinline__ void persist_body(const Params<R>& p) {
   }
   uint64_t segs = 0;
   if (item0 < p.n_items) {
-    Path<R, Trav::kColdLds, Trav::kLean, Trav::kNoRad> s;
+    Path<R, Trav::kColdLds, Trav::kLean, Trav::kNoRad, Trav::kThrLds> s;
     s.set_acc(mkv(R(0), R(0), R(0)));
     begin_item(p, s, item0);
     begin_sample<R, CAMX>(p, s);
@@ -1852,6 +1898,12 @@ constexpr size_t kWideLdsBudget = 40u << 10;  // bytes per 256-lane block: 4 blo
 static_assert(((size_t)RT_WIDE_LDS_STACK * kBlock * 4u + (size_t)RT_WIDE_TOP_N * kWTopStride + 1024u) *
                       RT_WIDE_WAVES_GLOBAL <= (160u << 10),
               "RT_WIDE_LDS_STACK / RT_WIDE_TOP_N do not fit RT_WIDE_WAVES_GLOBAL blocks per CU");
+// the same for the fp64 LL kernel over a tree in HBM at RT_WIDE_WAVES_GLOBAL_F64_LL blocks per CU: its LDS stack
+// entries, the fp16 top nodes and (RT_WIDE_THR_LDS_F64) the lanes' throughput
+static_assert(((size_t)RT_WIDE_LDS_STACK_F64 * kBlock * 4u + (size_t)RT_WIDE_TOP_N_F64 * sizeof(WNodeH) +
+               (RT_WIDE_THR_LDS_F64 ? 3u * kBlock * sizeof(double) : 0u) + 1024u) *
+                      RT_WIDE_WAVES_GLOBAL_F64_LL <= (160u << 10),
+              "RT_WIDE_LDS_STACK_F64 / RT_WIDE_TOP_N_F64 do not fit RT_WIDE_WAVES_GLOBAL_F64_LL blocks per CU");
 static_assert(RT_WIDE_TOP_N <= kWideTopMax && RT_WIDE_TOP_N_F64 <= kWideTopMax,
               "the scene compiler orders at most kWideTopMax top nodes first");
 template <class R>
