@@ -1111,11 +1111,8 @@ constexpr uint32_t kWNodeLdsStride = 144;
 // The WNode stride of 128 bytes put every node's row r on one of only two windows: lanes reading the top of the
 // tree serialised on the banks (C4 fp32: 43 G bank-conflict cycles per launch against 93 G of LDS activity,
 // r05fin4_c4_f32_pmc.json).
-#ifndef RT_WIDE_TOP_STRIDE
-#define RT_WIDE_TOP_STRIDE 112
-#endif
-constexpr uint32_t kWTopStride = RT_WIDE_TOP_STRIDE;
-static_assert(kWTopStride == 112 || kWTopStride == 128, "a top node is its 7 rows, optionally padded to 8");
+// (112 against the 128-byte stride measured the same time, 264.6 / 264.9 ms/frame, r06a; the conflicts: §4 of DESIGN.md)
+constexpr uint32_t kWTopStride = 112;
 #ifdef RT_SECTION_CLOCKS
 // development build (scripts/dev_wide_stats.py): wave-level counts of the wide kernels, per block
 // in LDS, added to g_wide_stats at the end: [0] node-loop iterations, [1] lanes in them, [2]

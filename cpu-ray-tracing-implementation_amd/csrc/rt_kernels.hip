@@ -50,15 +50,6 @@ constexpr int kBlock = 256;
 // background
 // RT_BG_SOLID_FAST (retired in round 6, always on): shade: nor against another solid background when |d| < 500 (the
 // test always hits)
-#ifndef RT_LLI_SHARED_TRIG  // shade LLI: one sincos for the isotropic and lambertian lanes of a material sample
-#define RT_LLI_SHARED_TRIG 1
-#endif
-#ifndef RT_WIDE_THR_LDS_F64  // the fp64 LL kernel over a tree in HBM keeps the path throughput in LDS (Path LT)
-#define RT_WIDE_THR_LDS_F64 1
-#endif
-#ifndef RT_LLI_THR_LDS  // the fp32 LLI volume kernel keeps the path throughput in LDS (Path LT)
-#define RT_LLI_THR_LDS 1
-#endif
 #ifndef RT_LINEAR_WAVES
 #define RT_LINEAR_WAVES 6
 #endif
@@ -888,7 +879,7 @@ __device__ bool shade(const Params<R>& p, PS& s, R t, uint32_t e, int32_t inst, 
             dir = from_light ? dl : dc;
           } else if (from_light) {
             dir = light_random(Lt, pw, u1, u2);
-          } else if constexpr (LLI && RT_LLI_SHARED_TRIG) {
+          } else if constexpr (LLI) {  // (C5 fp64 2,200 -> 2,185 ms/frame, fp32 1,094 -> 1,091, r06c)
             // the isotropic (on_sphere: phi = 2 pi u2) and lambertian (cosine: phi = 2 pi u1) lanes share one sincos
             R sp, cp;
             sincos2pi(iso ? u2 : u1, sp, cp);
@@ -995,7 +986,7 @@ struct LinearTrav {
   static constexpr bool kLean = false;  // (LLI lean: 7 waves 1,094 -> 1,117 ms/frame; 8 waves 48 B spilled, r06a)
   static constexpr bool kNoRad = VOL;
   static constexpr bool kColdLds = VOL;
-  static constexpr bool kThrLds = RT_LLI_THR_LDS && VOL && LLI && sizeof(R) == 4;  // (Path LT)
+  static constexpr bool kThrLds = VOL && LLI && sizeof(R) == 4;  // (Path LT: C5 fp32 1,091 -> 1,072 ms/frame, r06d)
   template <class PS>
   __device__ __forceinline__ static void run(const DevScene<R>& sc, const Node<R>*, const PS& s, Keys k,
                                              uint32_t*, R& t, uint32_t& e, int32_t& i, uint32_t&) {
@@ -1152,7 +1143,7 @@ struct WideTrav {
   // (Path LT) the fp64 LL kernel over a tree in HBM (C4): its throughput in LDS, 6 KB a block, for which its LDS stack
   // keeps 18 entries instead of 24: 339.2 -> 331.8 ms/frame, writes 16.4 -> 9.4 GB per launch (r06d). The fp64 NL
   // kernel over an LDS tree (C3) lost with it: 63.55 -> 68.08 ms/frame
-  static constexpr bool kThrLds = RT_WIDE_THR_LDS_F64 && sizeof(R) == 8 && !LDSN && LL;
+  static constexpr bool kThrLds = sizeof(R) == 8 && !LDSN && LL;
   static constexpr bool kTablesLds = false;
   static constexpr bool kLean = true;  // registers for the traversal (fewer spills)
   static constexpr bool kNoRad = true;
@@ -1899,9 +1890,9 @@ static_assert(((size_t)RT_WIDE_LDS_STACK * kBlock * 4u + (size_t)RT_WIDE_TOP_N *
                       RT_WIDE_WAVES_GLOBAL <= (160u << 10),
               "RT_WIDE_LDS_STACK / RT_WIDE_TOP_N do not fit RT_WIDE_WAVES_GLOBAL blocks per CU");
 // the same for the fp64 LL kernel over a tree in HBM at RT_WIDE_WAVES_GLOBAL_F64_LL blocks per CU: its LDS stack
-// entries, the fp16 top nodes and (RT_WIDE_THR_LDS_F64) the lanes' throughput
+// entries, the fp16 top nodes and the lanes' throughput (Path LT)
 static_assert(((size_t)RT_WIDE_LDS_STACK_F64 * kBlock * 4u + (size_t)RT_WIDE_TOP_N_F64 * sizeof(WNodeH) +
-               (RT_WIDE_THR_LDS_F64 ? 3u * kBlock * sizeof(double) : 0u) + 1024u) *
+               3u * kBlock * sizeof(double) + 1024u) *
                       RT_WIDE_WAVES_GLOBAL_F64_LL <= (160u << 10),
               "RT_WIDE_LDS_STACK_F64 / RT_WIDE_TOP_N_F64 do not fit RT_WIDE_WAVES_GLOBAL_F64_LL blocks per CU");
 static_assert(RT_WIDE_TOP_N <= kWideTopMax && RT_WIDE_TOP_N_F64 <= kWideTopMax,
@@ -2387,8 +2378,7 @@ int32_t rt_abi_version(void) { return RT_ABI_VERSION; }
 #define RT_STR2(x) #x
 #define RT_STR(x) RT_STR2(x)
 const char* rt_build_info(void) {
-  return "dev_only=" RT_STR(RT_DEV_ONLY) " wide_top_n=" RT_STR(RT_WIDE_TOP_N) " wide_top_stride=" RT_STR(
-      RT_WIDE_TOP_STRIDE) " wide_lds_stack=" RT_STR(RT_WIDE_LDS_STACK) " wide_waves_global=" RT_STR(RT_WIDE_WAVES_GLOBAL)
+  return "dev_only=" RT_STR(RT_DEV_ONLY) " wide_top_n=" RT_STR(RT_WIDE_TOP_N) " wide_lds_stack=" RT_STR(RT_WIDE_LDS_STACK) " wide_waves_global=" RT_STR(RT_WIDE_WAVES_GLOBAL)
 #ifdef RT_SECTION_CLOCKS
       " sections=1"
 #endif
