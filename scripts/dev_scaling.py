@@ -6,6 +6,7 @@ max over ranks per N.
     python scripts/dev_scaling.py [--config c2] [--worlds 1,2,4,8] [--steps 3]
 """
 import argparse
+import gc
 import json
 import os
 import sys
@@ -49,15 +50,18 @@ def main():
         per_rank, kern = [], []
         for r in range(world):
             stream = torch.cuda.current_stream(dev).cuda_stream
-            ctx.render_tiles(cam, params, all_tiles[r], out.data_ptr(), 1, stream)  # warmup
+            tl = abi.TileList(all_tiles[r])  # built once, as FrameSharding does (bench.py)
+            ctx.render_tiles(cam, params, tl, out.data_ptr(), 1, stream)  # warmup
             torch.cuda.synchronize(dev)
             ctx.set_timing(True)
             ctx.reset_counters()
             t0 = time.perf_counter()
+            gc.disable()  # (round 6: one rank's host time in a C3 8-rank run was 2-3x its kernel time)
             for _ in range(args.steps):
-                ctx.render_tiles(cam, params, all_tiles[r], out.data_ptr(), 1, stream)
+                ctx.render_tiles(cam, params, tl, out.data_ptr(), 1, stream)
             torch.cuda.synchronize(dev)
             per_rank.append((time.perf_counter() - t0) / args.steps * 1e3)
+            gc.enable()
             kern.append(ctx.stats().step_ms / args.steps)  # the persistent kernel alone (HIP events)
             ctx.set_timing(False)
         worst = max(per_rank)
