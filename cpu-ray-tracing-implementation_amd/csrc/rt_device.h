@@ -830,15 +830,15 @@ __device__ __forceinline__ bool aquad_t(const R* f, V<R> o, V<R> d, V<R> inv, R 
     t = th;
     return in_t & in_ab;
   }
-  if (!(tmin <= th && th <= tmax)) return false;
-  R pu = (comp<U>(o) + th * comp<U>(d)) - f[1];
-  R pv = (comp<W>(o) + th * comp<W>(d)) - f[2];
-  R a, b;
-  a = pu * f[3];  // the stored reciprocals 1/u_U, 1/v_V (fp64: within an ulp of pu / u_U)
-  b = pv * f[4];
-  if (!(R(0) <= a && a <= R(1) && R(0) <= b && b <= R(1))) return false;
+  // fp64 (round 6): the same without branches, as the flat program's quads: plain compares for t, the bit order for
+  // alpha and beta (the products with the stored reciprocals 1/u_U, 1/v_V, within an ulp of pu / u_U) (C5 fp64
+  // 2,121 -> 2,092 ms/frame, r06i)
+  const R a = fma((comp<U>(o) + th * comp<U>(d)) - f[1], f[3], R(0));
+  const R b = fma((comp<W>(o) + th * comp<W>(d)) - f[2], f[4], R(0));
+  const bool in_t = (th >= tmin) & (th <= tmax);
+  const uint64_t ua = (uint64_t)__double_as_longlong(a), ub = (uint64_t)__double_as_longlong(b);
   t = th;
-  return true;
+  return in_t & (ua <= 0x3FF0000000000000ull) & (ub <= 0x3FF0000000000000ull);
 }
 template <class R>
 __device__ __forceinline__ bool lin_quad_t(const LinRec<R>& r, V<R> o, V<R> d, V<R> inv, R tmin, R tmax, R& t) {
@@ -956,8 +956,8 @@ __device__ bool volume_t(const DevScene<R>& sc, const Volume<R>& v, V<R> wo, V<R
 
 // ------------------------------------------------------------------ traversal
 // world.hit(r, interval(0.001, inf), rec) (camera.h:198) as a stack machine.
-// excl_*: the surface the ray leaves (its previous hit); a planar primitive
-// cannot be re-hit from its own surface, a sphere only through its far side.
+// excl_*: the surface the ray leaves (its previous hit); in fp32 a planar primitive
+// cannot be re-hit from its own surface, a sphere only through its far side (fp64: no exclusion).
 #ifdef RT_SECTION_CLOCKS
 // development build: traversal counts (pops, node pops, primitive tests), summed over rays
 __device__ unsigned long long g_trace_totals[3];
@@ -987,7 +987,9 @@ __device__ void trace(const DevScene<R>& sc, const Node<R>* nodes, V<R> wo, V<R>
     g_trace_counts[2] += 1;
 #endif
     uint32_t ty = etype(e), i = epay(e);
-    bool self = (e == excl_e) && (cur == excl_i);
+    // (fp32 only: in fp64 the surface a ray leaves is re-hit at ~ulp(o) / |d.n|, below tmin unless the ray grazes it,
+    // when the reference's own test, which excludes nothing, re-hits it too -- the flat program's argument, round 6)
+    const bool self = sizeof(R) == 4 && (e == excl_e) && (cur == excl_i);
     R th;
     bool h;
     if (ty == E_QUAD) {
@@ -1447,11 +1449,12 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
       if (SPH && (!(TRI || QUAD) || ty == E_SPHERE)) {
         const WW b = PF ? a1 : pw(w + 1);
         w += 2;
-        hit = sphere_test(mkv(h.x, h.y, h.z), mkv(b.x, b.y, b.z), b.w, MOV, ro, rd, time, tmin, tmax, e == excl_e, th);
+        // (fp64 excludes nothing, as the reference: trace's note)
+        hit = sphere_test(mkv(h.x, h.y, h.z), mkv(b.x, b.y, b.z), b.w, MOV, ro, rd, time, tmin, tmax, !F64 && e == excl_e, th);
       } else if (TRI && (!QUAD || ty == E_TRI)) {
         const WW a = PF ? a1 : pw(w + 1), b = PF ? a2 : pw(w + 2);
         w += 3;
-        hit = e != excl_e && tri_test(mkv(h.x, h.y, h.z), mkv(a.x, a.y, a.z), mkv(b.x, b.y, b.z), ro, rd, tmin, tmax, th);
+        hit = (F64 || e != excl_e) && tri_test(mkv(h.x, h.y, h.z), mkv(a.x, a.y, a.z), mkv(b.x, b.y, b.z), ro, rd, tmin, tmax, th);
       } else if (QUAD) {
         const WW nD = PF ? a1 : pw(w + 1), qa = PF ? a2 : pw(w + 2), qb = pw(w + 3);
         // (no fp64 re-decision near edges here, unlike quad_t_near. Inline, its registers spilled the C4 fp32
@@ -1459,7 +1462,7 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
         // saved around it spilled the kernel's loop instead: 264.6 -> 307.5 ms/frame, for a C4 lit fp32 RMSE
         // (fp32 against fp64 over 400 tiles) of 1.71e-4 -> 1.30e-4 -- the rest are triangle edges and the
         // fp32 paths' own rounding (r06a))
-        hit = e != excl_e && quad_test(mkv(nD.x, nD.y, nD.z), nD.w, mkv(h.x, h.y, h.z), mkv(qa.x, qa.y, qa.z),
+        hit = (F64 || e != excl_e) && quad_test(mkv(nD.x, nD.y, nD.z), nD.w, mkv(h.x, h.y, h.z), mkv(qa.x, qa.y, qa.z),
                                        mkv(qb.x, qb.y, qb.z), ro, rd, tmin, tmax, th);
         w += 4;
       }
@@ -1593,6 +1596,8 @@ __device__ __forceinline__ bool trace_wide(const DevScene<R>& sc, const unsigned
       // LDS tree: a child's code is loaded when it is pushed (loading all four with the boxes keeps them
       // live through the slab tests and the sort, which spilled: C3 76.4 -> 81.5 ms/frame). Tree in HBM:
       // all four come with the boxes, one latency instead of one per push (C4 462 -> 421 ms/frame).
+      // (Round 6: the LDS tree's four codes in one 8-byte read after the sort spilled 16 B more: C3 fp64 62.4 -> 65.7,
+      // fp32 47.0 -> 49.4 ms/frame, r06i.)
       uint4 cc{};
       uint32_t k0, k1, k2, k3;
       if constexpr (kHalf) {
@@ -1681,13 +1686,13 @@ __device__ __forceinline__ void trace_linear(const DevScene<R>& sc, V<R> wo, V<R
     if (ty == E_QUAD) {
       if constexpr (sizeof(R) == 4)  // evaluated for every lane, excluded lanes masked (no branch)
         h = lin_quad_t(rec, o, d, inv, tmin, tmax, th) & !(op == excl_e && cur == excl_i);
-      else if (!(op == excl_e && cur == excl_i))
+      else  // fp64 excludes nothing, as the reference (trace's note)
         h = lin_quad_t(rec, o, d, inv, tmin, tmax, th);
     } else if (SPH && ty == E_SPHERE) {
       h = sphere_test(ld3(rec.f), ld3(rec.f + 4), rec.f[3], rec.aux != 0, o, d, time, tmin, tmax,
-                      op == excl_e && cur == excl_i, th);
+                      sizeof(R) == 4 && op == excl_e && cur == excl_i, th);
     } else if (TRI && ty == E_TRI) {
-      if (!(op == excl_e && cur == excl_i)) {
+      if (sizeof(R) == 8 || !(op == excl_e && cur == excl_i)) {
         Tri<R> tr;
         for (int q = 0; q < 3; q++) {
           tr.p0[q] = rec.f[q];
